@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""Encrypted-compare throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): one query against a shard of 1024
+documents per GPU, 16-dim features, n_bits = 6. One step = one pass of the
+whole encrypted path over the shard, all on the GPU:
+    pair features + quantize -> encrypt (D LWEs per pair) -> leveled dot
+    product with the quantized weights -> decrypt the accumulator ->
+    P-round exact bit extraction (P key switches + P bootstraps per pair)
+    -> decrypt the encrypted threshold bit -> local top-k
+and, for N > 1, the RCCL all-gather of the per-shard top-k (the only
+exchange step of the sharded search) plus the merge.
+Inputs (query, documents) are resident in HBM before the timed region.
+value = compares processed by all ranks / (max over ranks of the time).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RCCL = backend "nccl").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+for _p in (str(REPO / "fhe-icp_amd"), str(REPO)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "encrypted compares/sec (PBS/sec), 16-dim, 1/2/4/8 GPU; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
+F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--docs", type=int, default=1024, help="documents per GPU (shard size)")
+    ap.add_argument("--dim", type=int, default=16)
+    ap.add_argument("--n-bits", type=int, default=6)
+    ap.add_argument("--top-k", type=int, default=10)
+    ap.add_argument("--min-similarity", type=float, default=0.5)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-compares", type=int, default=16)
+    ap.add_argument("--cpu-rounds", type=int, default=2,
+                    help="bit-extraction rounds actually run per compare in the CPU sample")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def build_model(args):
+    from fheicp.model import FheLinearModel
+    from fheicp.datagen import training_pairs
+    X, y = training_pairs(args.dim, 1000, seed=args.seed + 1)
+    return FheLinearModel.fit(X, y, n_bits=args.n_bits)
+
+
+def shard(args, rank):
+    from fheicp.datagen import corpus
+    # global corpus of world*docs documents; this rank owns a contiguous range
+    q, docs = corpus(args.dim, args.docs, seed=args.seed + 100 + rank, query_seed=args.seed + 99)
+    return q, docs
+
+
+def br_flops_per_ct(p) -> float:
+    """Analytic f64 FLOPs of one blind rotation."""
+    M = p.N // 2
+    logm = int(np.log2(M))
+    fft = 5.0 * M * logm + 6.0 * M             # radix-2 complex FFT + twist
+    nf, ni = (p.k + 1) * p.pbs_level, p.k + 1
+    pointwise = 8.0 * nf * ni * M
+    return p.n * (nf * fft + ni * fft + pointwise)
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from fheicp import _lib
+    _lib.lib()  # loud failure if the HIP library is missing
+
+    model = build_model(args)
+    model.compile(key_seed=args.seed, device=local)
+    eng = model.engine
+    p = eng.params
+    P = model.msg_bits
+    from fheicp.model import threshold_int
+    T = threshold_int(model.qparams, args.min_similarity)
+
+    q_np, docs_np = shard(args, rank)
+    q_dev = torch.from_numpy(q_np).to(dev)
+    d_dev = torch.from_numpy(docs_np).to(dev)
+    B = docs_np.shape[0]
+    base_idx = rank * B
+
+    def step():
+        qx = model.quantize_dev(d_dev, q_dev)
+        acc, below = model.encrypted_acc(qx, T)
+        oa, oi = eng.topk(acc, below, args.top_k, base_idx)
+        if world > 1:
+            # the sharded search's one exchange: all-gather k (acc, idx) per rank
+            ga = [torch.empty_like(oa) for _ in range(world)]
+            gi = [torch.empty_like(oi) for _ in range(world)]
+            torch.distributed.all_gather(ga, oa)
+            torch.distributed.all_gather(gi, oi)
+            cat_a, cat_i = torch.cat(ga), torch.cat(gi)
+            # merge with the same (acc desc, idx asc) order: ranks own ascending
+            # contiguous index ranges, so position order == global index order
+            oa, pos = eng.topk(cat_a, (cat_i < 0).to(torch.int64), args.top_k, 0)
+            oi = torch.where(pos >= 0, cat_i[pos.clamp(min=0)], pos)
+        return acc, below, oa, oi
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    eng.profile(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        acc, below, oa, oi = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.profile(False)
+    br = eng.profile_read("blind_rotate")
+    ks = eng.profile_read("keyswitch")
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    compares = world * B * args.steps
+    value = compares / elapsed
+    ms_step = elapsed / args.steps * 1e3
+
+    # external-product (blind rotation) kernel roofline, from HIP events
+    avg_ms = br["total_ms"] / max(br["launches"], 1)
+    cts_per_launch = br["items"] / max(br["launches"], 1)
+    R = (p.k + 1) * p.pbs_level
+    bsk_bytes = p.n * R * (p.k + 1) * (p.N // 2) * 16
+    io_bytes = cts_per_launch * ((p.n + 1) * 8 + (p.k * p.N + 1) * 8 * 5)
+    alg_bytes = bsk_bytes + io_bytes
+    achieved_gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
+    flops = br_flops_per_ct(p) * cts_per_launch
+    achieved_tf = flops / (avg_ms * 1e-3) / 1e12
+    traffic = None
+    tj = REPO / "profiles" / "r01_br_traffic.json"
+    if tj.exists():
+        try:
+            traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "compares/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"batch compare 1 query x {B} encrypted docs per GPU, {args.dim}-dim, n_bits={args.n_bits} "
+                        f"(BASELINE configs[1]) + encrypted threshold (min_similarity {args.min_similarity}) "
+                        f"+ top-{args.top_k}" + (" + RCCL top-k all-gather" if world > 1 else ""),
+            "docs_per_gpu": B, "dim": args.dim, "n_bits": args.n_bits, "msg_bits_P": P,
+            "pbs_per_compare": P, "keyswitch_per_compare": P,
+            "params": p.as_dict(), "parallelism": f"shard{world}",
+        },
+        "pbs_per_sec": round(value * P, 1),
+        "roofline": {
+            "kernel": "k_blind_rotate (external products)",
+            "bound": "hbm",
+            "achieved": round(achieved_gbs, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "avg_launch_ms": round(avg_ms, 4),
+            "launches": br["launches"],
+            "cts_per_launch": cts_per_launch,
+            "alg_bytes_per_launch": int(alg_bytes),
+            "note": "algorithmic bytes = FFT-domain BSK once per launch + per-ct LWE I/O; the kernel is f64-VALU "
+                    "bound, see compute",
+            "compute": {"achieved_tflops_f64": round(achieved_tf, 2), "peak_tflops_f64": F64_VALU_PEAK_TFLOPS,
+                        "frac": round(achieved_tf / F64_VALU_PEAK_TFLOPS, 4)},
+        },
+        "keyswitch_ms_total": round(ks["total_ms"], 3),
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"], out["parity"] = cpu_leg(args, model, q_np, docs_np, acc, below, T)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
+    """The oracle, timed on the host cores (bounded sample), and the parity
+    check of the last timed step against the clear restatement."""
+    from oracle import quant_ref as Q
+    from oracle import tfhe_ref as R
+    X, y = __import__("fheicp.datagen", fromlist=["x"]).training_pairs(args.dim, 1000, seed=args.seed + 1)
+    oq = Q.fit_quantized_linear(X, y, args.n_bits)
+    Xp = Q.pair_features(q_np, docs_np)
+    acc_ref = Q.accumulate(oq, Q.quantize_input(oq, Xp))
+    acc = acc_dev.cpu().numpy()
+    below = below_dev.cpu().numpy()
+    scores_ref = Q.dequantize(oq, acc_ref)
+    parity = {
+        "compares_checked": int(len(acc)),
+        "acc_bit_exact": bool(np.array_equal(acc, acc_ref)),
+        "threshold_bit_exact": bool(np.array_equal(below, (scores_ref < args.min_similarity).astype(np.int64))),
+        "quant_params_equal": oq.to_json() == model.qparams.to_dict(),
+    }
+    # Oracle TFHE on C compares: encrypt + linear + decrypt, then r of the P
+    # bit-extraction rounds (identical work per round), extrapolated to P.
+    p = model.engine.params.as_dict()
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    C = args.cpu_compares
+    ref = R.RefTFHE(p, args.seed)
+    qx = Q.quantize_input(oq, Xp[:C])
+    t0 = time.perf_counter()
+    ct = ref.encrypt_ints(qx.reshape(-1), seed=5)
+    lin = ref.linear(ct, C, args.dim, oq.q_w, oq.const_term - T)
+    v = ref.decrypt_ints(lin)
+    t_lev = time.perf_counter() - t0
+    rounds = max(1, min(args.cpu_rounds, model.msg_bits))
+    Pb = model.msg_bits
+    t0 = time.perf_counter()
+    cv = lin.copy()
+    for i in range(rounds):
+        sh = cv << np.uint64(Pb - 1 - i)
+        sh[:, -1] += np.uint64(1 << 62)
+        small = ref.keyswitch(sh)
+        ref.pbs_const(small, 1 << (63 - Pb + i))
+    t_round = (time.perf_counter() - t0) / rounds
+    t_total = t_lev + t_round * Pb
+    parity["cpu_oracle_acc_matches"] = bool(np.array_equal(v + T, acc_ref[:C]))
+    base = {
+        "value": round(C / t_total, 4),
+        "unit": "compares/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{C} compares of the same workload on the exact C oracle (Karatsuba Z_2^64 TFHE, OpenMP "
+                  f"{cores} threads): encrypt+linear+decrypt timed fully, {rounds} of {Pb} bit-extraction rounds "
+                  f"(KS+PBS) timed and scaled to {Pb}",
+        "seconds": round(t_lev + t_round * rounds, 2),
+    }
+    # the reference's shipped CPU path (Concrete predict fhe="disable": clear
+    # quantized inference), numpy, single process
+    t0 = time.perf_counter()
+    reps = 200
+    for _ in range(reps):
+        Q.predict(oq, Xp)
+    t_clear = (time.perf_counter() - t0) / reps
+    base["clear_path_compares_per_s"] = round(len(Xp) / t_clear, 1)
+    return base, parity
+
+
+if __name__ == "__main__":
+    main()

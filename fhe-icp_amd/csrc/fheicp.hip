@@ -1,0 +1,1030 @@
+// libfheicp: MI355X-native TFHE engine for the encrypted pairwise compare of
+// shipstone-labs/fhe-icp. C ABI in include/fhe_icp.h; design in DESIGN.md.
+//
+// Kernels (one file so the whole engine is one code object):
+//   keygen:   k_keygen_secrets, k_keygen_bsk, k_keygen_ksk, k_bsk_to_fft
+//   client:   k_encrypt, k_decrypt
+//   server:   k_linear          (Concrete-ML _inference, leveled)
+//             k_keyswitch       (big -> small key, tiled GEMM-like)
+//             k_blind_rotate    (external products, f64 wave FFT)  <- hot
+//   search:   k_topk
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fhe_icp.h"
+#include "prng.h"
+#include "wave_fft.h"
+
+using namespace fhei;
+typedef uint64_t u64;
+
+// ============================================================ helpers ======
+__device__ __forceinline__ uint32_t modswitch_2n(u64 a, int log2n2) {
+  return (uint32_t)((((a >> (63 - log2n2)) + 1) >> 1) & ((1ull << log2n2) - 1));
+}
+
+// Closest multiple of 2^(64 - L*beta) of x, re-encoded as L balanced digits
+// packed offset-binary: digit of level lvl (1 = most significant) is
+// ((packed >> ((L - lvl) * beta)) & (B-1)) - B/2.  
+__device__ __forceinline__ u64 decompose_packed(u64 x, int beta, int L) {
+  const int prec = L * beta;
+  u64 r = ((x >> (63 - prec)) + 1) >> 1;
+  if (prec < 64) r &= ((1ull << prec) - 1);
+  int64_t v = (int64_t)r;
+  const int64_t B = (int64_t)1 << beta;
+  u64 packed = 0;
+  for (int l = L; l >= 1; --l) {
+    int64_t d = v & (B - 1);
+    v >>= beta;
+    if (d >= B / 2) {
+      d -= B;
+      v += 1;
+    }
+    packed |= (u64)(d + B / 2) << ((L - l) * beta);
+  }
+  return packed;
+}
+__device__ __forceinline__ int digit_of(u64 packed, int lvl, int beta, int L) {
+  const int64_t B = (int64_t)1 << beta;
+  return (int)((int64_t)((packed >> ((L - lvl) * beta)) & (u64)(B - 1)) - B / 2);
+}
+
+template <int NT>
+__device__ __forceinline__ u64 block_sum_u64(u64 v, u64* red) {
+  // wave reduce
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  u64 s = 0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+  __syncthreads();
+  return s;  // valid in thread 0
+}
+
+// ============================================================ keygen =======
+__global__ void k_keygen_secrets(ChaKey K, int n, int big, u64* s_small, u64* s_big) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) s_small[i] = stream_word(K, TAG_SK_SMALL, 0, (u64)i) & 1;
+  if (i < big) s_big[i] = stream_word(K, TAG_SK_GLWE, 0, (u64)i) & 1;
+}
+
+// One workgroup per GGSW row (i, r): GLWE_S(0) + s_small[i] * g_lvl on
+// component c_in. body = sum_j A_j * S_j (negacyclic, binary S) + E.
+__global__ void __launch_bounds__(256) k_keygen_bsk(ChaKey K, int N, int k, int L, int beta, int noise_bits,
+                                                    const u64* __restrict__ s_small, const u64* __restrict__ s_big,
+                                                    u64* __restrict__ bsk) {
+  extern __shared__ u64 shm[];
+  u64* A = shm;                                          // N
+  unsigned char* S = (unsigned char*)(shm + N);          // N
+  const int R = (k + 1) * L;
+  const int row = blockIdx.x;  // i * R + r
+  const int i = row / R, r = row % R;
+  const int c_in = r / L, lvl = r % L + 1;
+  u64* dst = bsk + (size_t)row * (k + 1) * N;
+  constexpr int MAXC = 8;  // N <= 2048 -> 8 coefficients per thread
+  u64 body[MAXC];
+  const int per = N / 256;
+  for (int q = 0; q < per; ++q) body[q] = 0;
+  for (int j = 0; j < k; ++j) {
+    const u64 sid = (u64)row * k + j;
+    for (int blk = threadIdx.x; blk < N / 8; blk += 256) {
+      u64 w[8];
+      stream_block(K, TAG_BSK_MASK, sid, (uint32_t)blk, w);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        A[8 * blk + q] = w[q];
+        dst[(size_t)j * N + 8 * blk + q] = w[q];
+      }
+    }
+    for (int t = threadIdx.x; t < N; t += 256) S[t] = (unsigned char)s_big[(size_t)j * N + t];
+    __syncthreads();
+    for (int v = 0; v < N; ++v) {
+      if (!S[v]) continue;  // uniform across the block
+      for (int q = 0; q < per; ++q) {
+        const int t = threadIdx.x + 256 * q;
+        body[q] += (t >= v) ? A[t - v] : (u64)0 - A[t - v + N];
+      }
+    }
+    __syncthreads();
+  }
+  for (int q = 0; q < per; ++q) {
+    const int t = threadIdx.x + 256 * q;
+    u64 b = body[q] + (u64)tuniform(stream_word(K, TAG_BSK_NOISE, (u64)row, (u64)t), noise_bits);
+    dst[(size_t)k * N + t] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_small[i]) dst[(size_t)c_in * N] += 1ull << (64 - lvl * beta);
+}
+
+// One workgroup per KSK row (i, l): LWE_{s_small}(s_big[i] * 2^(64 - (l+1) beta)).
+__global__ void __launch_bounds__(256) k_keygen_ksk(ChaKey K, int n, int KL, int kbeta, int noise_bits,
+                                                    const u64* __restrict__ s_small, const u64* __restrict__ s_big,
+                                                    u64* __restrict__ ksk) {
+  __shared__ u64 red[4];
+  const int row = blockIdx.x;  // i * KL + l
+  const int i = row / KL, l = row % KL;
+  u64* dst = ksk + (size_t)row * (n + 1);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < (n + 7) / 8; blk += 256) {
+    u64 w[8];
+    stream_block(K, TAG_KSK_MASK, (u64)row, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int t = 8 * blk + q;
+      if (t < n) {
+        dst[t] = w[q];
+        if (s_small[t]) part += w[q];
+      }
+    }
+  }
+  const u64 s = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    u64 b = s + (u64)tuniform(stream_word(K, TAG_KSK_NOISE, (u64)row, 0), noise_bits);
+    if (s_big[i]) b += 1ull << (64 - (l + 1) * kbeta);
+    dst[n] = b;
+  }
+}
+
+// One wave per polynomial: fold/twist, forward FFT, scale 1/M, store in the
+// [u][lane] order the blind rotation reads (coalesced 1 KiB per slot).
+template <int LOGM>
+__global__ void __launch_bounds__(64) k_bsk_to_fft(const u64* __restrict__ bsk, int npoly,
+                                                   const c64* __restrict__ tw, const c64* __restrict__ twist,
+                                                   c64* __restrict__ out) {
+  using F = WaveFFT<LOGM>;
+  constexpr int M = F::M, S = F::S;
+  __shared__ c64 lds[F::LDS_ELEMS];
+  const int poly = blockIdx.x, l = threadIdx.x;
+  if (poly >= npoly) return;
+  const u64* src = bsk + (size_t)poly * 2 * M;
+  c64 v[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) {
+    const int t = l + 64 * u;
+    const c64 a = {(double)(int64_t)src[t], (double)(int64_t)src[t + M]};
+    v[u] = cmul(a, twist[t]);
+  }
+  F::forward(v, tw, lds, l);
+  const double inv = 1.0 / (double)M;
+  c64* dst = out + (size_t)poly * M;
+#pragma unroll
+  for (int u = 0; u < S; ++u) dst[u * 64 + l] = {v[u].x * inv, v[u].y * inv};
+}
+
+// ============================================================ client =======
+// One workgroup (256 threads) per ciphertext of dimension `dim` (multiple of 8).
+__global__ void __launch_bounds__(256) k_encrypt(ChaKey K, int dim, int msg_bits, int noise_bits,
+                                                 const u64* __restrict__ s_big, const int64_t* __restrict__ msg,
+                                                 u64 id0, u64* __restrict__ ct) {
+  __shared__ u64 red[4];
+  const int64_t c = blockIdx.x;
+  const u64 id = id0 + (u64)c;
+  u64* o = ct + (size_t)c * (dim + 1);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 w[8];
+    stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[8 * blk + q] = w[q];
+      part += w[q] & (0 - s_big[8 * blk + q]);
+    }
+  }
+  const u64 s = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    const u64 e = (u64)tuniform(stream_word(K, TAG_ENC_NOISE, id, 0), noise_bits);
+    o[dim] = s + e + ((u64)msg[c] << (64 - msg_bits));
+  }
+}
+
+// mode 0: decode signed msg_bits integer; 1: bit (nearer 2^63); 2: raw phase
+__global__ void __launch_bounds__(256) k_decrypt(int dim, int msg_bits, int mode, const u64* __restrict__ s,
+                                                 const u64* __restrict__ ct, int64_t* __restrict__ out) {
+  __shared__ u64 red[4];
+  const int64_t c = blockIdx.x;
+  const u64* x = ct + (size_t)c * (dim + 1);
+  u64 part = 0;
+  for (int t = threadIdx.x; t < dim; t += 256) part += x[t] & (0 - s[t]);
+  const u64 sum = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    const u64 ph = x[dim] - sum;
+    int64_t r;
+    if (mode == 0) {
+      u64 q = ((ph >> (63 - msg_bits)) + 1) >> 1;
+      if (msg_bits < 64) q &= (1ull << msg_bits) - 1;
+      r = (q >> (msg_bits - 1)) ? (int64_t)q - ((int64_t)1 << msg_bits) : (int64_t)q;
+    } else if (mode == 1) {
+      r = (int64_t)(((ph + (1ull << 62)) >> 63) & 1);
+    } else {
+      r = (int64_t)ph;
+    }
+    out[c] = r;
+  }
+}
+
+// ============================================================ server =======
+// out[b][t] = sum_j w[j] ct[b][j][t] (+ cst * Delta on the body)
+__global__ void __launch_bounds__(256) k_linear(const u64* __restrict__ ct, int D, int W,
+                                                const int64_t* __restrict__ w, u64 cst_scaled,
+                                                u64* __restrict__ out) {
+  const int64_t b = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= W) return;
+  const u64* x = ct + (size_t)b * D * W + t;
+  u64 acc = 0;
+  for (int j = 0; j < D; ++j) acc += (u64)w[j] * x[(size_t)j * W];
+  if (t == W - 1) acc += cst_scaled;
+  out[(size_t)b * W + t] = acc;
+}
+
+// Key switch, tiled: a workgroup owns TC ciphertexts x 256 output columns.
+// Digits of (a_i << shift) for the TC ciphertexts are staged in LDS per
+// chunk of IC inputs; every KSK word read feeds TC multiply-adds.
+constexpr int KS_TC = 32, KS_IC = 32;
+__global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, int64_t count, int big, int n,
+                                                   int KL, int kbeta, int shift, u64 add_body,
+                                                   const u64* __restrict__ ksk, u64* __restrict__ out) {
+  __shared__ int8_t dig[KS_TC][KS_IC][8];
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.y * KS_TC;
+  const int nct = (int)min((int64_t)KS_TC, count - c0);
+  u64 acc[KS_TC];
+#pragma unroll
+  for (int q = 0; q < KS_TC; ++q) acc[q] = 0;
+  for (int i0 = 0; i0 < big; i0 += KS_IC) {
+    for (int e = threadIdx.x; e < KS_TC * KS_IC; e += 256) {
+      const int q = e / KS_IC, ii = e % KS_IC;
+      if (q < nct && i0 + ii < big) {
+        const u64 a = in[(size_t)(c0 + q) * (big + 1) + i0 + ii] << shift;
+        const u64 packed = decompose_packed(a, kbeta, KL);
+        for (int l = 1; l <= KL; ++l) dig[q][ii][l - 1] = (int8_t)digit_of(packed, l, kbeta, KL);
+      } else {
+        for (int l = 0; l < KL; ++l) dig[q][ii][l] = 0;
+      }
+    }
+    __syncthreads();
+    if (col <= n) {
+      const int iend = min(KS_IC, big - i0);
+      for (int ii = 0; ii < iend; ++ii) {
+        for (int l = 0; l < KL; ++l) {
+          const u64 kv = ksk[((size_t)(i0 + ii) * KL + l) * (n + 1) + col];
+#pragma unroll
+          for (int q = 0; q < KS_TC; ++q) acc[q] -= (u64)(int64_t)dig[q][ii][l] * kv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (col <= n) {
+    for (int q = 0; q < nct; ++q) {
+      u64 v = acc[q];
+      if (col == n) v += (in[(size_t)(c0 + q) * (big + 1) + big] << shift) + add_body;
+      out[(size_t)(c0 + q) * (n + 1) + col] = v;
+    }
+  }
+}
+
+// Blind rotation + sample extraction. One 64-lane wavefront (= workgroup)
+// per ciphertext; the GLWE accumulator ((K+1) x N u64) lives in LDS, the
+// external-product partial sums in registers.
+//   mode 0: out[c] = extracted LWE (phase ~ +-tv)
+//   mode 1: bit extraction epilogue: bit = trivial(tv) - extracted;
+//           ct_v[c] -= bit; refreshed[c] += bit; sign[c] = bit if sign != 0.
+template <int LOGM, int K>
+__global__ void __launch_bounds__(64) k_blind_rotate(const u64* __restrict__ small, int n, int L, int beta,
+                                                     const c64* __restrict__ bsk, const c64* __restrict__ tw,
+                                                     const c64* __restrict__ twist, u64 tv, int mode,
+                                                     u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                     u64* __restrict__ refreshed, u64* __restrict__ sign) {
+  using F = WaveFFT<LOGM>;
+  constexpr int M = F::M, S = F::S, N = 2 * M;
+  constexpr int LOG2N2 = LOGM + 2;
+  __shared__ u64 acc[(K + 1) * N];
+  __shared__ c64 lds[F::LDS_ELEMS];
+  const int l = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const u64* sm = small + (size_t)c * (n + 1);
+  const int R = (K + 1) * L;
+
+  // ACC = X^{-b~} * (0, .., 0, TV)
+  const uint32_t bt = modswitch_2n(sm[n], LOG2N2);
+  for (int t = l; t < N; t += 64) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[j * N + t] = 0;
+    const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
+    acc[K * N + t] = idx < (uint32_t)N ? tv : (u64)0 - tv;
+  }
+  __syncthreads();
+
+  for (int i = 0; i < n; ++i) {
+    const uint32_t ai = modswitch_2n(sm[i], LOG2N2);
+    if (ai == 0) continue;
+    c64 outv[K + 1][S];
+#pragma unroll
+    for (int o = 0; o <= K; ++o)
+#pragma unroll
+      for (int u = 0; u < S; ++u) outv[o][u] = {0.0, 0.0};
+    const c64* G = bsk + (size_t)i * R * (K + 1) * M;
+#pragma unroll
+    for (int cc = 0; cc <= K; ++cc) {
+      const u64* f = acc + cc * N;
+      u64 p0[S], p1[S];
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const int t0 = l + 64 * u, t1 = t0 + M;
+        uint32_t i0 = (uint32_t)(t0 - (int)ai) & (2 * N - 1);
+        uint32_t i1 = (uint32_t)(t1 - (int)ai) & (2 * N - 1);
+        const u64 r0 = i0 < (uint32_t)N ? f[i0] : (u64)0 - f[i0 - N];
+        const u64 r1 = i1 < (uint32_t)N ? f[i1] : (u64)0 - f[i1 - N];
+        p0[u] = decompose_packed(r0 - f[t0], beta, L);
+        p1[u] = decompose_packed(r1 - f[t1], beta, L);
+      }
+      for (int lvl = 1; lvl <= L; ++lvl) {
+        c64 v[S];
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+          const c64 d = {(double)digit_of(p0[u], lvl, beta, L), (double)digit_of(p1[u], lvl, beta, L)};
+          v[u] = cmul(d, twist[l + 64 * u]);
+        }
+        F::forward(v, tw, lds, l);
+        const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
+#pragma unroll
+        for (int o = 0; o <= K; ++o)
+#pragma unroll
+          for (int u = 0; u < S; ++u) cmac(outv[o][u], v[u], g[o * M + u * 64 + l]);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o <= K; ++o) {
+      F::inverse(outv[o], tw, lds, l);
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const int t0 = l + 64 * u;
+        const c64 z = cmulc(outv[o][u], twist[t0]);
+        acc[o * N + t0] += f64_to_torus(z.x);
+        acc[o * N + t0 + M] += f64_to_torus(z.y);
+      }
+    }
+    __syncthreads();
+  }
+
+  // sample extract coefficient 0 -> LWE under s_big (dim K*N)
+  const int W = K * N + 1;
+  for (int j = 0; j < K; ++j) {
+    for (int t = l; t < N; t += 64) {
+      const u64 a = (t == 0) ? acc[j * N] : (u64)0 - acc[j * N + N - t];
+      const size_t pos = (size_t)c * W + j * N + t;
+      if (mode == 0) {
+        out[pos] = a;
+      } else {
+        const u64 bit = (u64)0 - a;
+        ct_v[pos] -= bit;
+        refreshed[pos] += bit;
+        if (sign) sign[pos] = bit;
+      }
+    }
+  }
+  if (l == 0) {
+    const size_t pos = (size_t)c * W + K * N;
+    const u64 b = acc[K * N];
+    if (mode == 0) {
+      out[pos] = b;
+    } else {
+      const u64 bit = tv - b;
+      ct_v[pos] -= bit;
+      refreshed[pos] += bit;
+      if (sign) sign[pos] = bit;
+    }
+  }
+}
+
+// Client-side input path of batch_operations.py:226/:273 + Concrete-ML's
+// input quantizer, fused: X = query (.) doc in the operands' dtype (numpy
+// promotion), then q = clip(rint(X / s + zp), qmin, qmax) in float64.
+// IEEE division and rint make this bit-identical to numpy.
+template <typename QT, typename DT>
+__global__ void k_pair_quantize(const QT* __restrict__ query, const DT* __restrict__ docs, int64_t B, int D,
+                                double scale, double zp, double qmin, double qmax, int64_t* __restrict__ qx) {
+  using RT = decltype(QT() * DT());  // numpy promotion of the element-wise product
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * D) return;
+  const RT x = query ? (RT)query[e % D] * (RT)docs[e] : (RT)docs[e];
+  double q = rint((double)x / scale + zp);
+  q = fmin(fmax(q, qmin), qmax);
+  qx[e] = (int64_t)q;
+}
+
+// score[b] = out_scale * double(acc[b])  (UniformQuantizer.dequant, zp 0)
+__global__ void k_dequantize(const int64_t* __restrict__ acc, int64_t B, double out_scale, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) out[i] = out_scale * (double)acc[i];
+}
+
+// acc_out[b] = v[b] + T
+__global__ void k_add_scalar(const int64_t* __restrict__ v, int64_t B, int64_t T, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) out[i] = v[i] + T;
+}
+
+// Single-workgroup top-k by (acc desc, idx asc) over entries not below the
+// threshold. k passes; pass p selects the largest key strictly smaller than
+// the key chosen in pass p-1 (keys are unique because indices are).
+__global__ void __launch_bounds__(1024) k_topk(const int64_t* __restrict__ accv, const int64_t* __restrict__ below,
+                                               int64_t B, int64_t base_idx, int kk, int64_t* __restrict__ oa,
+                                               int64_t* __restrict__ oi) {
+  __shared__ int64_t sa[16], si[16];
+  __shared__ int64_t last_a, last_i;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) {
+    last_a = INT64_MAX;
+    last_i = -1;
+  }
+  __syncthreads();
+  for (int p = 0; p < kk; ++p) {
+    const int64_t la = last_a, li = last_i;
+    int64_t ba = INT64_MIN, bi = -1;
+    for (int64_t x = tid; x < B; x += 1024) {
+      if (below && below[x]) continue;
+      const int64_t a = accv[x];
+      // strictly after (la, li) in (acc desc, idx asc) order
+      const bool after = (a < la) || (a == la && x > li);
+      if (!after) continue;
+      if (bi < 0 || a > ba || (a == ba && x < bi)) {
+        ba = a;
+        bi = x;
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t oa2 = __shfl_down(ba, off, 64), oi2 = __shfl_down(bi, off, 64);
+      if (oi2 >= 0 && (bi < 0 || oa2 > ba || (oa2 == ba && oi2 < bi))) {
+        ba = oa2;
+        bi = oi2;
+      }
+    }
+    if (lane == 0) {
+      sa[w] = ba;
+      si[w] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t fa = INT64_MIN, fi = -1;
+      for (int q = 0; q < 16; ++q) {
+        if (si[q] >= 0 && (fi < 0 || sa[q] > fa || (sa[q] == fa && si[q] < fi))) {
+          fa = sa[q];
+          fi = si[q];
+        }
+      }
+      oa[p] = fi >= 0 ? fa : INT64_MIN;
+      oi[p] = fi >= 0 ? fi + base_idx : -1;
+      if (fi >= 0) {
+        last_a = fa;
+        last_i = fi;
+      } else {
+        last_a = INT64_MIN;  // nothing left: every later pass finds nothing
+        last_i = INT64_MAX;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================ host =========
+struct ProfAcc {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  double ms = 0;
+  int64_t launches = 0, items = 0;
+};
+
+struct fhe_ctx {
+  fhe_params p{};
+  int device = -1;
+  std::string err;
+  bool keys = false;
+  u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr;
+  c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr;
+  // workspace
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  bool prof = false;
+  ProfAcc prof_br, prof_ks;
+};
+
+static std::mutex g_err_mu;
+static std::string g_err;
+
+static int fail(fhe_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(ctx, x)                                                                          \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) return fail(ctx, FHE_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static int ilog2i(int x) {
+  int r = 0;
+  while ((1 << r) < x) ++r;
+  return r;
+}
+
+static int validate(const fhe_params* p, std::string& why) {
+  if (!p) { why = "null params"; return -1; }
+  if (!(p->N == 256 || p->N == 512 || p->N == 1024 || p->N == 2048)) { why = "N must be 256/512/1024/2048"; return -1; }
+  if (p->k < 1 || p->k > 2) { why = "k must be 1 or 2"; return -1; }
+  if (p->N == 2048 && p->k != 1) { why = "N=2048 requires k=1"; return -1; }
+  if (p->n < 1 || p->n > 4096) { why = "n out of range"; return -1; }
+  if (p->pbs_level < 1 || p->pbs_level > 8 || p->pbs_base_log < 1 || p->pbs_level * p->pbs_base_log > 62) {
+    why = "pbs decomposition out of range"; return -1;
+  }
+  if (p->ks_level < 1 || p->ks_level > 8 || p->ks_base_log < 1 || p->ks_base_log > 7 ||
+      p->ks_level * p->ks_base_log > 62) {
+    why = "ks decomposition out of range (base_log <= 7 for int8 digits)"; return -1;
+  }
+  if (p->msg_bits < 2 || p->msg_bits > 40) { why = "msg_bits must be in [2, 40]"; return -1; }
+  if (p->lwe_noise_bits < 0 || p->lwe_noise_bits > 60 || p->glwe_noise_bits < 0 || p->glwe_noise_bits > 60) {
+    why = "noise bits out of range"; return -1;
+  }
+  return 0;
+}
+
+extern "C" {
+
+size_t fhe_bsk_words(const fhe_params* p) {
+  return (size_t)p->n * (p->k + 1) * p->pbs_level * (p->k + 1) * p->N;
+}
+size_t fhe_ksk_words(const fhe_params* p) { return (size_t)p->k * p->N * p->ks_level * (p->n + 1); }
+size_t fhe_big_lwe_words(const fhe_params* p) { return (size_t)p->k * p->N + 1; }
+size_t fhe_small_lwe_words(const fhe_params* p) { return (size_t)p->n + 1; }
+
+const char* fhe_last_error(const fhe_ctx* ctx) {
+  if (ctx) return ctx->err.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_err.c_str();
+}
+
+int fhe_get_params(const fhe_ctx* ctx, fhe_params* out) {
+  if (!ctx || !out) return FHE_E_ARG;
+  *out = ctx->p;
+  return FHE_OK;
+}
+
+int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
+  std::string why;
+  if (!out) return fail(nullptr, FHE_E_ARG, "out is null");
+  *out = nullptr;
+  if (validate(params, why)) return fail(nullptr, FHE_E_ARG, why);
+  fhe_ctx* ctx = new fhe_ctx();
+  ctx->p = *params;
+  ctx->device = device;
+  if (device >= 0) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+      delete ctx;
+      return fail(nullptr, FHE_E_DEVICE, "no HIP device " + std::to_string(device));
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+      delete ctx;
+      return fail(nullptr, FHE_E_DEVICE, "hipSetDevice failed");
+    }
+    const int N = params->N, M = N / 2;
+    std::vector<c64> tw(M / 2), twist(M);
+    for (int x = 0; x < M / 2; ++x) {
+      const long double ang = 2.0L * 3.14159265358979323846264338327950288L * (long double)x / (long double)M;
+      tw[x] = {(double)cosl(ang), (double)sinl(ang)};
+    }
+    for (int t = 0; t < M; ++t) {
+      const long double ang = 3.14159265358979323846264338327950288L * (long double)t / (long double)N;
+      twist[t] = {(double)cosl(ang), (double)sinl(ang)};
+    }
+    if (hipMalloc(&ctx->tw, sizeof(c64) * tw.size()) != hipSuccess ||
+        hipMalloc(&ctx->twist, sizeof(c64) * twist.size()) != hipSuccess ||
+        hipMemcpy(ctx->tw, tw.data(), sizeof(c64) * tw.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->twist, twist.data(), sizeof(c64) * twist.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      fhe_ctx_destroy(ctx);
+      return fail(nullptr, FHE_E_DEVICE, "table upload failed");
+    }
+  }
+  *out = ctx;
+  return FHE_OK;
+}
+
+static void free_ev(ProfAcc& a) {
+  for (auto& e : a.ev) {
+    hipEventDestroy(e.first);
+    hipEventDestroy(e.second);
+  }
+  a.ev.clear();
+}
+
+void fhe_ctx_destroy(fhe_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->device >= 0) {
+    hipSetDevice(ctx->device);
+    hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk);
+    hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
+    free_ev(ctx->prof_br);
+    free_ev(ctx->prof_ks);
+  }
+  delete ctx;
+}
+
+int fhe_set_msg_bits(fhe_ctx* ctx, int32_t msg_bits) {
+  if (!ctx) return fail(nullptr, FHE_E_ARG, "null ctx");
+  fhe_params q = ctx->p;
+  q.msg_bits = msg_bits;
+  std::string why;
+  if (validate(&q, why)) return fail(ctx, FHE_E_ARG, why);
+  ctx->p = q;
+  return FHE_OK;
+}
+
+static int need_device(fhe_ctx* ctx) {
+  if (!ctx) return fail(nullptr, FHE_E_ARG, "null ctx");
+  if (ctx->device < 0) return fail(ctx, FHE_E_DEVICE, "host-only context");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, FHE_E_DEVICE, "hipSetDevice failed");
+  return FHE_OK;
+}
+static int need_keys(fhe_ctx* ctx) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (!ctx->keys) return fail(ctx, FHE_E_STATE, "no keys: call fhe_keygen or fhe_import_keys");
+  return FHE_OK;
+}
+
+static int alloc_keys(fhe_ctx* ctx) {
+  const fhe_params& p = ctx->p;
+  if (ctx->s_small) return FHE_OK;
+  HIPCHK(ctx, hipMalloc(&ctx->s_small, 8 * (size_t)p.n));
+  HIPCHK(ctx, hipMalloc(&ctx->s_big, 8 * (size_t)p.k * p.N));
+  HIPCHK(ctx, hipMalloc(&ctx->bsk, 8 * fhe_bsk_words(&p)));
+  HIPCHK(ctx, hipMalloc(&ctx->ksk, 8 * fhe_ksk_words(&p)));
+  HIPCHK(ctx, hipMalloc(&ctx->bsk_fft, sizeof(c64) * fhe_bsk_words(&p) / 2));
+  return FHE_OK;
+}
+
+static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
+  const fhe_params& p = ctx->p;
+  const int npoly = (int)(fhe_bsk_words(&p) / p.N);
+  switch (p.N) {
+    case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
+    case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
+    case 1024: hipLaunchKernelGGL(k_bsk_to_fft<9>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
+    case 2048: hipLaunchKernelGGL(k_bsk_to_fft<10>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
+  }
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (!h_key) return fail(ctx, FHE_E_ARG, "null key");
+  rc = alloc_keys(ctx);
+  if (rc) return rc;
+  const fhe_params& p = ctx->p;
+  hipStream_t st = (hipStream_t)stream;
+  ChaKey K;
+  memcpy(K.w, h_key, 32);
+  const int big = p.k * p.N;
+  const int mx = std::max(p.n, big);
+  hipLaunchKernelGGL(k_keygen_secrets, dim3((mx + 255) / 256), dim3(256), 0, st, K, p.n, big, ctx->s_small, ctx->s_big);
+  const int rows_bsk = p.n * (p.k + 1) * p.pbs_level;
+  const size_t shm = 8 * (size_t)p.N + p.N;
+  hipLaunchKernelGGL(k_keygen_bsk, dim3(rows_bsk), dim3(256), shm, st, K, p.N, p.k, p.pbs_level, p.pbs_base_log,
+                     p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk);
+  hipLaunchKernelGGL(k_keygen_ksk, dim3(big * p.ks_level), dim3(256), 0, st, K, p.n, p.ks_level, p.ks_base_log,
+                     p.lwe_noise_bits, ctx->s_small, ctx->s_big, ctx->ksk);
+  HIPCHK(ctx, hipGetLastError());
+  rc = convert_bsk(ctx, st);
+  if (rc) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  ctx->keys = true;
+  return FHE_OK;
+}
+
+int fhe_keygen(fhe_ctx* ctx, uint64_t seed, void* stream) {
+  ChaKey K = key_from_seed(seed);
+  return fhe_keygen_key(ctx, K.w, stream);
+}
+
+int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64_t* h_bsk, uint64_t* h_ksk) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  const fhe_params& p = ctx->p;
+  HIPCHK(ctx, hipDeviceSynchronize());
+  if (h_s_small) HIPCHK(ctx, hipMemcpy(h_s_small, ctx->s_small, 8 * (size_t)p.n, hipMemcpyDeviceToHost));
+  if (h_s_big) HIPCHK(ctx, hipMemcpy(h_s_big, ctx->s_big, 8 * (size_t)p.k * p.N, hipMemcpyDeviceToHost));
+  if (h_bsk) HIPCHK(ctx, hipMemcpy(h_bsk, ctx->bsk, 8 * fhe_bsk_words(&p), hipMemcpyDeviceToHost));
+  if (h_ksk) HIPCHK(ctx, hipMemcpy(h_ksk, ctx->ksk, 8 * fhe_ksk_words(&p), hipMemcpyDeviceToHost));
+  return FHE_OK;
+}
+
+int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
+                    const uint64_t* h_ksk) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (!h_s_small || !h_s_big || !h_bsk || !h_ksk) return fail(ctx, FHE_E_ARG, "all four key buffers are required");
+  rc = alloc_keys(ctx);
+  if (rc) return rc;
+  const fhe_params& p = ctx->p;
+  HIPCHK(ctx, hipMemcpy(ctx->s_small, h_s_small, 8 * (size_t)p.n, hipMemcpyHostToDevice));
+  HIPCHK(ctx, hipMemcpy(ctx->s_big, h_s_big, 8 * (size_t)p.k * p.N, hipMemcpyHostToDevice));
+  HIPCHK(ctx, hipMemcpy(ctx->bsk, h_bsk, 8 * fhe_bsk_words(&p), hipMemcpyHostToDevice));
+  HIPCHK(ctx, hipMemcpy(ctx->ksk, h_ksk, 8 * fhe_ksk_words(&p), hipMemcpyHostToDevice));
+  rc = convert_bsk(ctx, nullptr);
+  if (rc) return rc;
+  HIPCHK(ctx, hipDeviceSynchronize());
+  ctx->keys = true;
+  return FHE_OK;
+}
+
+int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_t seed, uint64_t id0,
+                      uint64_t* d_ct, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || (count > 0 && (!d_msg || !d_ct))) return fail(ctx, FHE_E_ARG, "bad encrypt arguments");
+  if (count == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  ChaKey K = key_from_seed(seed);
+  hipLaunchKernelGGL(k_encrypt, dim3((unsigned)count), dim3(256), 0, (hipStream_t)stream, K, p.k * p.N, p.msg_bits,
+                     p.glwe_noise_bits, ctx->s_big, d_msg, id0, d_ct);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+static int decrypt_mode(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, int64_t* d_out, int mode, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || (count > 0 && (!d_ct || !d_out))) return fail(ctx, FHE_E_ARG, "bad decrypt arguments");
+  if (count == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  hipLaunchKernelGGL(k_decrypt, dim3((unsigned)count), dim3(256), 0, (hipStream_t)stream, p.k * p.N, p.msg_bits,
+                     mode, ctx->s_big, d_ct, d_out);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+int fhe_decrypt_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, int64_t* d_out, void* stream) {
+  return decrypt_mode(ctx, d_ct, count, d_out, 0, stream);
+}
+int fhe_decrypt_bits_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, int64_t* d_out, void* stream) {
+  return decrypt_mode(ctx, d_ct, count, d_out, 1, stream);
+}
+int fhe_phase_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, uint64_t* d_out, void* stream) {
+  return decrypt_mode(ctx, d_ct, count, (int64_t*)d_out, 2, stream);
+}
+
+int fhe_linear_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                     uint64_t* d_out, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_ct || !d_w || !d_out))) return fail(ctx, FHE_E_ARG, "bad linear arguments");
+  if (B == 0) return FHE_OK;
+  if (B > 65535) return fail(ctx, FHE_E_ARG, "linear batch > 65535: split the call");
+  const fhe_params& p = ctx->p;
+  const int W = p.k * p.N + 1;
+  hipLaunchKernelGGL(k_linear, dim3((W + 255) / 256, (unsigned)B), dim3(256), 0, (hipStream_t)stream, d_ct, D, W, d_w,
+                     ((u64)cst) << (64 - p.msg_bits), d_out);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+static void prof_begin(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t* e1) {
+  *e1 = nullptr;
+  if (!ctx->prof) return;
+  hipEvent_t e0;
+  hipEventCreate(&e0);
+  hipEventCreate(e1);
+  hipEventRecord(e0, st);
+  a.ev.push_back({e0, *e1});
+}
+static void prof_end(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t e1, int64_t items) {
+  if (!ctx->prof || !e1) return;
+  hipEventRecord(e1, st);
+  a.launches += 1;
+  a.items += items;
+}
+
+int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
+                        uint64_t* d_small, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || shift < 0 || shift > 63 || (count > 0 && (!d_big || !d_small)))
+    return fail(ctx, FHE_E_ARG, "bad keyswitch arguments");
+  if (count == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t tiles = (count + KS_TC - 1) / KS_TC;
+  if (tiles > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
+  hipEvent_t e1;
+  prof_begin(ctx, ctx->prof_ks, st, &e1);
+  hipLaunchKernelGGL(k_keyswitch, dim3((p.n + 1 + 255) / 256, (unsigned)tiles), dim3(256), 0, st, d_big, count,
+                     p.k * p.N, p.n, p.ks_level, p.ks_base_log, shift, add_body, ctx->ksk, d_small);
+  prof_end(ctx, ctx->prof_ks, st, e1, count);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t tv, int mode, uint64_t* out,
+                     uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, hipStream_t st) {
+  const fhe_params& p = ctx->p;
+  hipEvent_t e1;
+  prof_begin(ctx, ctx->prof_br, st, &e1);
+  const dim3 g((unsigned)count), b(64);
+#define BR(LOGM, K)                                                                                           \
+  hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
+                     ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
+  if (p.N == 256 && p.k == 1) BR(7, 1);
+  else if (p.N == 256 && p.k == 2) BR(7, 2);
+  else if (p.N == 512 && p.k == 1) BR(8, 1);
+  else if (p.N == 512 && p.k == 2) BR(8, 2);
+  else if (p.N == 1024 && p.k == 1) BR(9, 1);
+  else if (p.N == 1024 && p.k == 2) BR(9, 2);
+  else if (p.N == 2048 && p.k == 1) BR(10, 1);
+  else return fail(ctx, FHE_E_ARG, "unsupported (N, k)");
+#undef BR
+  prof_end(ctx, ctx->prof_br, st, e1, count);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t tv, uint64_t* d_out, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || (count > 0 && (!d_small || !d_out))) return fail(ctx, FHE_E_ARG, "bad pbs arguments");
+  if (count == 0) return FHE_OK;
+  return launch_br(ctx, d_small, count, tv, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+static int ensure_ws(fhe_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->ws_bytes) return FHE_OK;
+  if (ctx->ws) {
+    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+  }
+  HIPCHK(ctx, hipMalloc(&ctx->ws, bytes));
+  ctx->ws_bytes = bytes;
+  return FHE_OK;
+}
+
+// bit extraction driver; `small` is caller-provided scratch (count x (n+1))
+static int bit_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_ref, uint64_t* d_sign,
+                       uint64_t* small, hipStream_t st) {
+  const fhe_params& p = ctx->p;
+  const int P = p.msg_bits;
+  HIPCHK(ctx, hipMemsetAsync(d_ref, 0, 8 * (size_t)count * fhe_big_lwe_words(&p), st));
+  for (int i = 0; i < P; ++i) {
+    int rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - 1 - i, 1ull << 62, small, st);
+    if (rc) return rc;
+    const u64 tv = 1ull << (63 - P + i);
+    rc = launch_br(ctx, small, count, tv, 1, nullptr, d_ct_v, d_ref, (i == P - 1) ? d_sign : nullptr, st);
+    if (rc) return rc;
+  }
+  return FHE_OK;
+}
+
+int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_refreshed, uint64_t* d_sign,
+                          void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || (count > 0 && (!d_ct_v || !d_refreshed || !d_sign)))
+    return fail(ctx, FHE_E_ARG, "bad bit-extract arguments");
+  if (count == 0) return FHE_OK;
+  rc = ensure_ws(ctx, 8 * (size_t)count * fhe_small_lwe_words(&ctx->p));
+  if (rc) return rc;
+  return bit_extract(ctx, d_ct_v, count, d_refreshed, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream);
+}
+
+int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                      int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_acc || !d_below)))
+    return fail(ctx, FHE_E_ARG, "bad compare arguments");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
+  // workspace: inputs (B*D big) | ct_v (B big) | refreshed (B big) | sign (B big) | small (B) | v (B)
+  const size_t bytes = 8 * ((size_t)B * D * Wb + 3 * (size_t)B * Wb + (size_t)B * Ws + (size_t)B);
+  rc = ensure_ws(ctx, bytes);
+  if (rc) return rc;
+  u64* cin = (u64*)ctx->ws;
+  u64* ctv = cin + (size_t)B * D * Wb;
+  u64* ref = ctv + (size_t)B * Wb;
+  u64* sgn = ref + (size_t)B * Wb;
+  u64* small = sgn + (size_t)B * Wb;
+  int64_t* v = (int64_t*)(small + (size_t)B * Ws);
+  rc = fhe_encrypt_batch(ctx, d_qx, B * D, enc_seed, id0, cin, stream);
+  if (rc) return rc;
+  for (int64_t b0 = 0; b0 < B; b0 += 65535) {
+    const int64_t nb = std::min<int64_t>(65535, B - b0);
+    rc = fhe_linear_batch(ctx, cin + (size_t)b0 * D * Wb, nb, D, d_w, cst - T, ctv + (size_t)b0 * Wb, stream);
+    if (rc) return rc;
+  }
+  // The score comes from the leveled accumulator ciphertext (noise ~2^20,
+  // as in the reference's leveled Concrete circuit); the PBS chain then
+  // computes the encrypted threshold bit [acc < T] exactly.
+  rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
+  if (rc) return rc;
+  rc = bit_extract(ctx, ctv, B, ref, sgn, small, st);
+  if (rc) return rc;
+  rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_quantize_pairs(fhe_ctx* ctx, const void* d_query, int32_t query_is_f64, const void* d_docs,
+                       int32_t docs_is_f64, int64_t B, int32_t D, double scale, int64_t zero_point, int64_t qmin,
+                       int64_t qmax, int64_t* d_qx, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_docs || !d_qx)) || !(scale > 0) || qmin > qmax)
+    return fail(ctx, FHE_E_ARG, "bad quantize arguments");
+  if (B == 0) return FHE_OK;
+  const int64_t total = B * D;
+  const dim3 g((unsigned)((total + 255) / 256)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  const double z = (double)zero_point, lo = (double)qmin, hi = (double)qmax;
+#define QLAUNCH(QT, DT) \
+  hipLaunchKernelGGL((k_pair_quantize<QT, DT>), g, b, 0, st, (const QT*)d_query, (const DT*)d_docs, B, D, scale, z, lo, hi, d_qx)
+  if (query_is_f64 && docs_is_f64) QLAUNCH(double, double);
+  else if (query_is_f64) QLAUNCH(double, float);
+  else if (docs_is_f64) QLAUNCH(float, double);
+  else QLAUNCH(float, float);
+#undef QLAUNCH
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_dequantize(fhe_ctx* ctx, const int64_t* d_acc, int64_t B, double out_scale, double* d_score, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && (!d_acc || !d_score))) return fail(ctx, FHE_E_ARG, "bad dequantize arguments");
+  if (B == 0) return FHE_OK;
+  hipLaunchKernelGGL(k_dequantize, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_acc, B,
+                     out_scale, d_score);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_topk(fhe_ctx* ctx, const int64_t* d_acc, const int64_t* d_below, int64_t B, int64_t base_idx, int32_t k,
+             int64_t* d_out_acc, int64_t* d_out_idx, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (B < 0 || k < 0 || (k > 0 && (!d_out_acc || !d_out_idx)) || (B > 0 && !d_acc))
+    return fail(ctx, FHE_E_ARG, "bad topk arguments");
+  if (k == 0) return FHE_OK;
+  hipLaunchKernelGGL(k_topk, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_acc, d_below, B, base_idx, k, d_out_acc,
+                     d_out_idx);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_profile_enable(fhe_ctx* ctx, int enable) {
+  if (!ctx) return fail(nullptr, FHE_E_ARG, "null ctx");
+  ctx->prof = enable != 0;
+  return FHE_OK;
+}
+
+int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (!kernel) return fail(ctx, FHE_E_ARG, "null kernel name");
+  ProfAcc* a = nullptr;
+  if (!strcmp(kernel, "blind_rotate")) a = &ctx->prof_br;
+  else if (!strcmp(kernel, "keyswitch")) a = &ctx->prof_ks;
+  else return fail(ctx, FHE_E_ARG, "unknown kernel name");
+  double ms = 0;
+  for (auto& e : a->ev) {
+    HIPCHK(ctx, hipEventSynchronize(e.second));
+    float x = 0;
+    HIPCHK(ctx, hipEventElapsedTime(&x, e.first, e.second));
+    ms += x;
+  }
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = a->launches;
+  if (items) *items = a->items;
+  free_ev(*a);
+  a->launches = 0;
+  a->items = 0;
+  return FHE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// ChaCha20 (RFC 8439) counter-mode streams and TUniform noise — device side.
+//
+// Every random word of the scheme (secret keys, key masks, key noise,
+// encryption masks and noise) is addressed as stream(tag, id)[w]: u64 word w
+// is ChaCha20 block floor(w/8) (block counter) of (key, nonce = {tag,
+// id_lo, id_hi}), 32-bit output words 2(w%8) and 2(w%8)+1. Addressing by
+// (tag, id, w) makes generation embarrassingly parallel and reproducible
+// across any launch geometry.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fhei {
+
+enum StreamTag : uint32_t {
+  TAG_SK_SMALL = 1,
+  TAG_SK_GLWE = 2,
+  TAG_BSK_MASK = 3,
+  TAG_BSK_NOISE = 4,
+  TAG_KSK_MASK = 5,
+  TAG_KSK_NOISE = 6,
+  TAG_ENC_MASK = 7,
+  TAG_ENC_NOISE = 8,
+};
+
+struct ChaKey {
+  uint32_t w[8];
+};
+
+__host__ __device__ __forceinline__ uint32_t rotl32(uint32_t a, int b) { return (a << b) | (a >> (32 - b)); }
+
+#define FHEI_QR(a, b, c, d)                       \
+  a += b; d ^= a; d = rotl32(d, 16);              \
+  c += d; b ^= c; b = rotl32(b, 12);              \
+  a += b; d ^= a; d = rotl32(d, 8);               \
+  c += d; b ^= c; b = rotl32(b, 7);
+
+// One ChaCha20 block; out[16] little-endian 32-bit words.
+__host__ __device__ __forceinline__ void chacha20_block(const ChaKey& K, uint32_t counter, uint32_t tag,
+                                                        uint64_t id, uint32_t out[16]) {
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = K.w[0], x5 = K.w[1], x6 = K.w[2], x7 = K.w[3];
+  uint32_t x8 = K.w[4], x9 = K.w[5], x10 = K.w[6], x11 = K.w[7];
+  uint32_t x12 = counter, x13 = tag, x14 = (uint32_t)id, x15 = (uint32_t)(id >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    FHEI_QR(x0, x4, x8, x12) FHEI_QR(x1, x5, x9, x13) FHEI_QR(x2, x6, x10, x14) FHEI_QR(x3, x7, x11, x15)
+    FHEI_QR(x0, x5, x10, x15) FHEI_QR(x1, x6, x11, x12) FHEI_QR(x2, x7, x8, x13) FHEI_QR(x3, x4, x9, x14)
+  }
+  out[0] = x0 + 0x61707865u; out[1] = x1 + 0x3320646eu; out[2] = x2 + 0x79622d32u; out[3] = x3 + 0x6b206574u;
+  out[4] = x4 + K.w[0]; out[5] = x5 + K.w[1]; out[6] = x6 + K.w[2]; out[7] = x7 + K.w[3];
+  out[8] = x8 + K.w[4]; out[9] = x9 + K.w[5]; out[10] = x10 + K.w[6]; out[11] = x11 + K.w[7];
+  out[12] = x12 + counter; out[13] = x13 + tag; out[14] = x14 + (uint32_t)id; out[15] = x15 + (uint32_t)(id >> 32);
+}
+#undef FHEI_QR
+
+// Eight consecutive u64 words [8*blk, 8*blk+8) of stream (tag, id).
+__host__ __device__ __forceinline__ void stream_block(const ChaKey& K, uint32_t tag, uint64_t id, uint32_t blk,
+                                                      uint64_t w[8]) {
+  uint32_t o[16];
+  chacha20_block(K, blk, tag, id, o);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = (uint64_t)o[2 * j] | ((uint64_t)o[2 * j + 1] << 32);
+}
+
+__host__ __device__ __forceinline__ uint64_t stream_word(const ChaKey& K, uint32_t tag, uint64_t id, uint64_t w) {
+  uint32_t o[16];
+  chacha20_block(K, (uint32_t)(w >> 3), tag, id, o);
+  const int j = (int)(w & 7);
+  return (uint64_t)o[2 * j] | ((uint64_t)o[2 * j + 1] << 32);
+}
+
+// TUniform(b): uniform on [-2^b, 2^b] with the two endpoints at half weight.
+__host__ __device__ __forceinline__ int64_t tuniform(uint64_t w, int b) {
+  const uint64_t bits = w & ((2ull << (b + 1)) - 1);  // b + 2 bits
+  return (int64_t)((bits >> 1) + (bits & 1)) - ((int64_t)1 << b);
+}
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// 64-bit seed -> 256-bit ChaCha key (for reproducible tests and benches; a
+// deployment passes 32 bytes from the OS CSPRNG via fhe_*_key entry points).
+__host__ __device__ __forceinline__ ChaKey key_from_seed(uint64_t seed) {
+  ChaKey K;
+  uint64_t x = seed;
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t v = splitmix64(x);
+    K.w[2 * i] = (uint32_t)v;
+    K.w[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+  return K;
+}
+
+}  // namespace fhei

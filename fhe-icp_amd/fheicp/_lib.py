@@ -1,0 +1,95 @@
+"""ctypes binding of libfheicp.so (include/fhe_icp.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).
+There is no fallback: if the shared object is missing or fails to load, every
+entry point raises, so a GPU run can never silently degrade to a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libfheicp.so"
+
+FHE_OK = 0
+ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOMEM"}
+
+PARAM_FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
+                "lwe_noise_bits", "glwe_noise_bits", "msg_bits")
+
+
+class FheParams(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in PARAM_FIELDS]
+
+
+# (name, restype, argtypes) for every symbol declared in include/fhe_icp.h
+_vp = C.c_void_p
+_i64 = C.c_int64
+_u64 = C.c_uint64
+_i32 = C.c_int32
+_P = C.POINTER(FheParams)
+_CTXP = C.c_void_p
+SIGNATURES = [
+    ("fhe_ctx_create", C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p)]),
+    ("fhe_ctx_destroy", None, [_CTXP]),
+    ("fhe_last_error", C.c_char_p, [_CTXP]),
+    ("fhe_get_params", C.c_int, [_CTXP, _P]),
+    ("fhe_set_msg_bits", C.c_int, [_CTXP, _i32]),
+    ("fhe_bsk_words", C.c_size_t, [_P]),
+    ("fhe_ksk_words", C.c_size_t, [_P]),
+    ("fhe_big_lwe_words", C.c_size_t, [_P]),
+    ("fhe_small_lwe_words", C.c_size_t, [_P]),
+    ("fhe_keygen", C.c_int, [_CTXP, _u64, _vp]),
+    ("fhe_keygen_key", C.c_int, [_CTXP, C.POINTER(C.c_uint32), _vp]),
+    ("fhe_export_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
+    ("fhe_import_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
+    ("fhe_encrypt_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _vp, _vp]),
+    ("fhe_decrypt_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
+    ("fhe_decrypt_bits_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
+    ("fhe_phase_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
+    ("fhe_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+    ("fhe_keyswitch_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
+    ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
+    ("fhe_bit_extract_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp, _vp]),
+    ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
+    ("fhe_quantize_pairs", C.c_int, [_CTXP, _vp, _i32, _vp, _i32, _i64, _i32, C.c_double, _i64, _i64, _i64, _vp, _vp]),
+    ("fhe_dequantize", C.c_int, [_CTXP, _vp, _i64, C.c_double, _vp, _vp]),
+    ("fhe_topk", C.c_int, [_CTXP, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    ("fhe_profile_enable", C.c_int, [_CTXP, C.c_int]),
+    ("fhe_profile_read", C.c_int, [_CTXP, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64), C.POINTER(_i64)]),
+]
+
+_lib = None
+
+
+class FheError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libfheicp.so (raises FheError if it is absent or broken)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise FheError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+        try:
+            L = C.CDLL(str(LIB_PATH))
+        except OSError as e:  # pragma: no cover - depends on the machine
+            raise FheError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc != FHE_OK:
+        msg = lib().fhe_last_error(ctx)
+        msg = msg.decode() if msg else ""
+        raise FheError(f"{ERRORS.get(rc, rc)}: {msg}")
+
+
+def params_struct(d: dict) -> FheParams:
+    return FheParams(**{f: int(d[f]) for f in PARAM_FIELDS})

@@ -1,0 +1,197 @@
+"""Device-side engine: one libfheicp context per GPU, torch tensors as buffers.
+
+PyTorch is plumbing here (device allocation, streams, host<->device copies);
+all arithmetic runs in the HIP kernels of libfheicp.so. Ciphertext words are
+stored in int64 tensors (bit patterns of the u64 words).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .params import SchemeParams
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    assert t.is_contiguous(), "buffers must be contiguous"
+    return C.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Engine:
+    """A TFHE context on one MI355X (gfx950) device."""
+
+    def __init__(self, params: SchemeParams, device: int | str | torch.device = 0):
+        if not torch.cuda.is_available():
+            raise _lib.FheError("fheicp.Engine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.params = params
+        self._L = _lib.lib()
+        self._P = _lib.params_struct(params.as_dict())
+        h = C.c_void_p()
+        _lib.check(self._L.fhe_ctx_create(C.byref(self._P), self.device.index, C.byref(h)))
+        self._ctx = h
+        self.big = params.k * params.N
+        self.W = self.big + 1
+        self.Ws = params.n + 1
+        self.has_keys = False
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._L.fhe_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int) -> None:
+        _lib.check(rc, self._ctx)
+
+    def set_msg_bits(self, P: int) -> None:
+        self._chk(self._L.fhe_set_msg_bits(self._ctx, int(P)))
+        self.params = self.params.with_msg_bits(P)
+
+    @property
+    def msg_bits(self) -> int:
+        return self.params.msg_bits
+
+    # ---------------------------------------------------------------- keys --
+    def keygen(self, seed: int) -> None:
+        with torch.cuda.device(self.device):
+            self._chk(self._L.fhe_keygen(self._ctx, C.c_uint64(seed), _stream(self.device)))
+        self.has_keys = True
+
+    def export_keys(self) -> dict:
+        p = self.params
+        out = {
+            "s_small": np.zeros(p.n, np.uint64),
+            "s_big": np.zeros(self.big, np.uint64),
+            "bsk": np.zeros(self._L.fhe_bsk_words(C.byref(self._P)), np.uint64),
+            "ksk": np.zeros(self._L.fhe_ksk_words(C.byref(self._P)), np.uint64),
+        }
+        self._chk(self._L.fhe_export_keys(self._ctx, *(C.c_void_p(out[k].ctypes.data)
+                                                       for k in ("s_small", "s_big", "bsk", "ksk"))))
+        return out
+
+    def import_keys(self, keys: dict) -> None:
+        arrs = [np.ascontiguousarray(keys[k], dtype=np.uint64) for k in ("s_small", "s_big", "bsk", "ksk")]
+        self._chk(self._L.fhe_import_keys(self._ctx, *(C.c_void_p(a.ctypes.data) for a in arrs)))
+        self.has_keys = True
+
+    # ------------------------------------------------------------- buffers --
+    def empty_big(self, count: int) -> torch.Tensor:
+        return torch.empty((count, self.W), dtype=torch.int64, device=self.device)
+
+    def empty_small(self, count: int) -> torch.Tensor:
+        return torch.empty((count, self.Ws), dtype=torch.int64, device=self.device)
+
+    def to_dev(self, a, dtype=torch.int64) -> torch.Tensor:
+        if isinstance(a, torch.Tensor):
+            return a.to(self.device, dtype=dtype).contiguous()
+        a = np.ascontiguousarray(a)
+        if a.dtype == np.uint64:
+            a = a.view(np.int64)
+        return torch.from_numpy(a).to(self.device, dtype=dtype).contiguous()
+
+    # ------------------------------------------------------ client / server --
+    def encrypt(self, msg, seed: int, id0: int = 0) -> torch.Tensor:
+        m = self.to_dev(msg).reshape(-1)
+        ct = self.empty_big(m.numel())
+        self._chk(self._L.fhe_encrypt_batch(self._ctx, _ptr(m), m.numel(), C.c_uint64(seed), C.c_uint64(id0),
+                                            _ptr(ct), _stream(self.device)))
+        return ct
+
+    def decrypt(self, ct: torch.Tensor) -> torch.Tensor:
+        n = ct.numel() // self.W
+        out = torch.empty(n, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_decrypt_batch(self._ctx, _ptr(ct), n, _ptr(out), _stream(self.device)))
+        return out
+
+    def decrypt_bits(self, ct: torch.Tensor) -> torch.Tensor:
+        n = ct.numel() // self.W
+        out = torch.empty(n, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_decrypt_bits_batch(self._ctx, _ptr(ct), n, _ptr(out), _stream(self.device)))
+        return out
+
+    def phase(self, ct: torch.Tensor) -> torch.Tensor:
+        n = ct.numel() // self.W
+        out = torch.empty(n, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_phase_batch(self._ctx, _ptr(ct), n, _ptr(out), _stream(self.device)))
+        return out
+
+    def linear(self, ct: torch.Tensor, B: int, D: int, w, cst: int) -> torch.Tensor:
+        wd = self.to_dev(w)
+        out = self.empty_big(B)
+        self._chk(self._L.fhe_linear_batch(self._ctx, _ptr(ct), B, D, _ptr(wd), int(cst), _ptr(out),
+                                           _stream(self.device)))
+        return out
+
+    def keyswitch(self, ct: torch.Tensor, shift: int = 0, add_body: int = 0) -> torch.Tensor:
+        n = ct.numel() // self.W
+        out = self.empty_small(n)
+        self._chk(self._L.fhe_keyswitch_batch(self._ctx, _ptr(ct), n, shift, C.c_uint64(add_body), _ptr(out),
+                                              _stream(self.device)))
+        return out
+
+    def pbs(self, small: torch.Tensor, tv: int) -> torch.Tensor:
+        n = small.numel() // self.Ws
+        out = self.empty_big(n)
+        self._chk(self._L.fhe_pbs_batch(self._ctx, _ptr(small), n, C.c_uint64(tv), _ptr(out), _stream(self.device)))
+        return out
+
+    def bit_extract(self, ct_v: torch.Tensor):
+        """Consumes ct_v; returns (refreshed, sign) ciphertexts."""
+        n = ct_v.numel() // self.W
+        ref = self.empty_big(n)
+        sign = self.empty_big(n)
+        self._chk(self._L.fhe_bit_extract_batch(self._ctx, _ptr(ct_v), n, _ptr(ref), _ptr(sign),
+                                                _stream(self.device)))
+        return ref, sign
+
+    def compare(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc_seed: int, id0: int = 0):
+        """Fused encrypt -> linear -> bit extraction -> decrypt for B pairs.
+
+        Returns (acc int64[B], below int64[B])."""
+        B, D = q_x.shape
+        acc = torch.empty(B, dtype=torch.int64, device=self.device)
+        below = torch.empty(B, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_compare_batch(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T),
+                                            C.c_uint64(enc_seed), C.c_uint64(id0), _ptr(acc), _ptr(below),
+                                            _stream(self.device)))
+        return acc, below
+
+    def topk(self, acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx: int = 0):
+        oa = torch.empty(k, dtype=torch.int64, device=self.device)
+        oi = torch.empty(k, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_topk(self._ctx, _ptr(acc), _ptr(below), acc.numel(), base_idx, k, _ptr(oa), _ptr(oi),
+                                   _stream(self.device)))
+        return oa, oi
+
+    # --------------------------------------------------------- measurement --
+    def profile(self, enable: bool) -> None:
+        self._chk(self._L.fhe_profile_enable(self._ctx, int(enable)))
+
+    def profile_read(self, kernel: str) -> dict:
+        ms = C.c_double()
+        nl = C.c_int64()
+        items = C.c_int64()
+        self._chk(self._L.fhe_profile_read(self._ctx, kernel.encode(), C.byref(ms), C.byref(nl), C.byref(items)))
+        return {"total_ms": ms.value, "launches": nl.value, "items": items.value}
+
+
+def u64(t: torch.Tensor) -> np.ndarray:
+    """Device int64 tensor -> host uint64 array (bit pattern)."""
+    return t.detach().cpu().numpy().view(np.uint64)

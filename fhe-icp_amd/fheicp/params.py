@@ -1,0 +1,91 @@
+"""Parameter sets and the noise model that selects them.
+
+The reference delegates parameter choice to Concrete's optimizer inside
+``model.compile`` (fhe_similarity.py:120), sized from a 10-sample inputset.
+Here parameters are chosen from the WORST-CASE accumulator width P (every
+representable quantized input), so no input can overflow the encoding.
+
+Security anchors (not re-estimated here; no lattice estimator offline):
+  * small LWE (n = 887, TUniform(46)) and
+  * GLWE with k*N = 2048 and TUniform(17)
+are the pairs tfhe-rs publishes as 128-bit secure for its TUniform
+parameter sets; this build uses k = 2, N = 1024 (same k*N).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import asdict, dataclass, replace
+
+
+@dataclass(frozen=True)
+class SchemeParams:
+    n: int = 887
+    k: int = 2
+    N: int = 1024
+    pbs_base_log: int = 15
+    pbs_level: int = 2
+    ks_base_log: int = 4
+    ks_level: int = 4
+    lwe_noise_bits: int = 46
+    glwe_noise_bits: int = 17
+    msg_bits: int = 16
+
+    def as_dict(self) -> dict:
+        return asdict(self)
+
+    def with_msg_bits(self, P: int) -> "SchemeParams":
+        return replace(self, msg_bits=int(P))
+
+
+# Bootstrap gadget by message width (checked by noise_report()).
+PBS_GADGETS = ((18, 15, 2), (22, 12, 3), (24, 10, 4), (26, 8, 5), (28, 7, 6))
+
+
+def params_for_bits(P: int) -> SchemeParams:
+    for pmax, beta, lvl in PBS_GADGETS:
+        if P <= pmax:
+            return SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
+    raise ValueError(f"accumulator width P={P} exceeds the supported 28 bits")
+
+
+# A tiny, INSECURE set with the same structure, for fast functional tests.
+TOY = SchemeParams(n=64, k=2, N=256, pbs_base_log=15, pbs_level=2, ks_base_log=4, ks_level=4,
+                   lwe_noise_bits=46, glwe_noise_bits=17, msg_bits=8)
+
+
+def _tuniform_var(b: int) -> float:
+    """Variance of TUniform(b): (2^(2b+1) + 1) / 6."""
+    return (2.0 ** (2 * b + 1) + 1.0) / 6.0
+
+
+def noise_report(p: SchemeParams) -> dict:
+    """Variance model (relative to the 2^64 torus) of one bit-extraction round.
+
+    Worst round is i = 1, where the PBS output noise of bit 0 is amplified by
+    2^(P-2) before the sign bootstrap reads it.
+    """
+    q2 = 2.0 ** 128
+    s2_bsk = _tuniform_var(p.glwe_noise_bits) / q2
+    s2_ksk = _tuniform_var(p.lwe_noise_bits) / q2
+    B = 2.0 ** p.pbs_base_log
+    rows = p.pbs_level * (p.k + 1) * p.N
+    br_key = p.n * rows * (B * B + 2) / 12.0 * s2_bsk
+    br_round = p.n * (1 + p.k * p.N / 2) / (12.0 * B ** (2 * p.pbs_level))
+    v_pbs = br_key + br_round
+    Bk = 2.0 ** p.ks_base_log
+    v_ks = p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk
+    v_ks += p.k * p.N / 2 * (2.0 ** (-2 * p.ks_level * p.ks_base_log)) / 12.0
+    v_ms = (p.n / 2 + 1) / 12.0 / (2.0 * p.N) ** 2
+    v_amp = v_pbs * 4.0 ** (p.msg_bits - 2)
+    v_total = v_amp + v_ks + v_ms
+    sigma = math.sqrt(v_total)
+    margin_sigmas = 0.25 / sigma
+    return {
+        "log2_sigma_pbs": 0.5 * math.log2(v_pbs),
+        "log2_sigma_ks": 0.5 * math.log2(v_ks),
+        "log2_sigma_ms": 0.5 * math.log2(v_ms),
+        "log2_sigma_total": math.log2(sigma),
+        "margin_sigmas": margin_sigmas,
+        # two-sided Gaussian tail at the 1/4-torus decision margin
+        "log2_pfail_per_pbs": math.log2(max(math.erfc(margin_sigmas / math.sqrt(2)), 1e-300)),
+    }

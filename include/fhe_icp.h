@@ -1,0 +1,170 @@
+/*
+ * fhe_icp.h — C ABI of libfheicp.so, the MI355X (gfx950) engine behind the
+ * encrypted pairwise compare of shipstone-labs/fhe-icp.
+ *
+ * Boundary. The reference reaches its hot path through a Concrete-ML
+ * estimator object: FHESimilarityModel.model is a
+ * concrete.ml.sklearn.LinearRegression (fhe_similarity.py:88-90) whose
+ * .predict(X, fhe=...) is called at fhe_similarity.py:151 (fhe="execute",
+ * encrypted), fhe_similarity.py:167 and batch_operations.py:233, :276
+ * (clear). Everything BELOW that predict call (quantize -> encrypt -> leveled
+ * dot product -> decrypt -> dequantize, concrete-python 2.10.0's runtime) is
+ * replaced by the entry points below; the Python estimator in
+ * fhe-icp_amd/fheicp/sklearn.py keeps the reference-facing API. The binding a
+ * maintainer adds on the reference side is shown in INTEGRATION.md.
+ *
+ * Conventions.
+ *  - Every function returns 0 on success and a negative FHE_E_* code on
+ *    failure; fhe_last_error(ctx) (or NULL ctx) returns the message.
+ *  - Pointers named d_* are DEVICE pointers on the context's device
+ *    (caller-owned, e.g. torch tensors); pointers named h_* are host memory.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream). All
+ *    launches are asynchronous on that stream unless documented otherwise.
+ *  - One context per device; calls on one context must be externally
+ *    serialised (same contract as the single-threaded reference callers).
+ *  - Ciphertexts are little-endian u64 arrays. An LWE ciphertext of
+ *    dimension d is [a_0 .. a_{d-1}, b] (d+1 words), phase = b - <a, s>
+ *    modulo 2^64. "Big" ciphertexts use dimension k*N, "small" ones n.
+ *  - Integer messages are encoded at Delta = 2^(64 - msg_bits).
+ */
+#ifndef FHE_ICP_H
+#define FHE_ICP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FHE_OK 0
+#define FHE_E_ARG (-1)      /* invalid argument / unsupported parameters */
+#define FHE_E_DEVICE (-2)   /* HIP runtime error or no device */
+#define FHE_E_STATE (-3)    /* keys not generated / imported */
+#define FHE_E_NOMEM (-4)
+
+/* Scheme parameters. Same field order as the oracle's. */
+typedef struct fhe_params {
+  int32_t n;               /* small LWE dimension (blind-rotation length) */
+  int32_t k;               /* GLWE dimension (1 or 2) */
+  int32_t N;               /* polynomial size: 256, 512, 1024 or 2048 */
+  int32_t pbs_base_log;    /* bootstrap gadget base log */
+  int32_t pbs_level;       /* bootstrap gadget levels (1..8) */
+  int32_t ks_base_log;     /* key-switch base log */
+  int32_t ks_level;        /* key-switch levels */
+  int32_t lwe_noise_bits;  /* TUniform bound, small LWE and KSK */
+  int32_t glwe_noise_bits; /* TUniform bound, GLWE, BSK and big-key LWE */
+  int32_t msg_bits;        /* P: message width of the accumulator encoding */
+} fhe_params;
+
+typedef struct fhe_ctx fhe_ctx;
+
+/* ---- context -------------------------------------------------------------
+ * Replaces the state Concrete builds in LinearRegression.compile()
+ * (fhe_similarity.py:120: circuit + keys held on the CPU heap). device < 0
+ * creates a host-only context (size queries, error strings; no kernels). */
+int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out);
+void fhe_ctx_destroy(fhe_ctx* ctx);
+const char* fhe_last_error(const fhe_ctx* ctx);
+int fhe_get_params(const fhe_ctx* ctx, fhe_params* out);
+/* Change P (msg_bits) without regenerating keys (keys do not depend on P). */
+int fhe_set_msg_bits(fhe_ctx* ctx, int32_t msg_bits);
+
+/* sizes in u64 words of the exported key material */
+size_t fhe_bsk_words(const fhe_params* params);
+size_t fhe_ksk_words(const fhe_params* params);
+size_t fhe_big_lwe_words(const fhe_params* params);   /* k*N + 1 */
+size_t fhe_small_lwe_words(const fhe_params* params); /* n + 1 */
+
+/* ---- keys ----------------------------------------------------------------
+ * Replaces Concrete keygen inside compile() (fhe_similarity.py:120) and the
+ * key material FHEKeyManager.generate_keys means to persist
+ * (key_management.py:112-191). Deterministic in `seed` (ChaCha20 streams,
+ * DESIGN.md §3.1); fhe_keygen_key takes a full 256-bit ChaCha key. */
+int fhe_keygen(fhe_ctx* ctx, uint64_t seed, void* stream);
+int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream);
+/* Host copies of the canonical key material; any pointer may be NULL.
+ * s_small: n words (0/1); s_big: k*N words (0/1); bsk: fhe_bsk_words
+ * (coefficient domain, [i][row][component][coef]); ksk: fhe_ksk_words
+ * ([i][level][n+1]). Synchronous. */
+int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64_t* h_bsk, uint64_t* h_ksk);
+int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
+                    const uint64_t* h_ksk);
+
+/* ---- client side: encrypt / decrypt --------------------------------------
+ * Replaces the per-sample encrypt/decrypt of predict(fhe="execute")
+ * (fhe_similarity.py:151). Ciphertext c uses stream id (id0 + c). */
+int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_t seed, uint64_t id0,
+                      uint64_t* d_ct, void* stream);
+/* round(phase / Delta) as signed msg_bits-bit integers */
+int fhe_decrypt_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, int64_t* d_out, void* stream);
+/* 1 iff phase is nearer 2^63 than 0 (decrypts a sign/bit ciphertext) */
+int fhe_decrypt_bits_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, int64_t* d_out, void* stream);
+/* raw phases (tests / noise measurement) */
+int fhe_phase_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, uint64_t* d_out, void* stream);
+
+/* ---- server side -----------------------------------------------------------
+ * The leveled circuit of Concrete-ML LinearRegression._inference:
+ *   out[b] = sum_j d_w[j] * ct[b, j] + trivial(cst * Delta),
+ * ct: B x D big ciphertexts (row-major), d_w: D int64 (device). */
+int fhe_linear_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                     uint64_t* d_out, void* stream);
+/* big -> small key switch of (ct << shift) + add_body (shift/add used by the
+ * bit extraction; pass 0, 0 for a plain key switch) */
+int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
+                        uint64_t* d_small, void* stream);
+/* Programmable bootstrap with the constant test vector `tv` (output phase
+ * ~ +tv if the input phase is in [0, 2^63), ~ -tv otherwise), sample-
+ * extracted under the big key. d_small: count x (n+1); d_out: count x (kN+1). */
+int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t tv, uint64_t* d_out,
+                  void* stream);
+/* Exact LSB-first bit extraction of the msg_bits-bit value v encrypted in
+ * d_ct_v (consumed). d_refreshed receives a fresh encryption of v (sum of
+ * the bit ciphertexts), d_sign the ciphertext of the top bit ([v < 0] at
+ * 2^63). msg_bits key-switches and bootstraps per ciphertext. */
+int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_refreshed, uint64_t* d_sign,
+                          void* stream);
+
+/* ---- fused compare / search ------------------------------------------------
+ * One call per batch of B (query, document) pairs — the batched replacement
+ * of the per-document loop at batch_operations.py:268-279 and of
+ * compare_encrypted (batch_operations.py:206-238):
+ *   encrypt q_x (B x D) -> linear with d_w and cst - T -> bit extraction ->
+ *   decrypt. d_acc[b] = the decrypted accumulator (exact int64, = Concrete's
+ *   q_x @ q_w - zp*sum(q_w) + q_b), d_below[b] = 1 iff acc < T (decrypted
+ *   encrypted threshold bit; acc >= T <=> score >= min_similarity).
+ * Uses context-owned workspace (grown on demand; not graph-capturable). */
+int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                      int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream);
+
+/* ---- clear pre/post-processing on the device ----------------------------
+ * Pair features and Concrete-ML's input quantizer in one pass:
+ * X[b, j] = query[j] * docs[b, j] in numpy's promoted dtype (the query may be
+ * f64, batch_operations.py:260; stored docs are f32, :178), or X = docs when
+ * d_query is NULL; then q = clip(rint(X / scale + zero_point), qmin, qmax)
+ * in float64 (concrete-ml UniformQuantizer.quant). Bit-identical to numpy. */
+int fhe_quantize_pairs(fhe_ctx* ctx, const void* d_query, int32_t query_is_f64, const void* d_docs,
+                       int32_t docs_is_f64, int64_t B, int32_t D, double scale, int64_t zero_point, int64_t qmin,
+                       int64_t qmax, int64_t* d_qx, void* stream);
+/* score[b] = out_scale * (double)acc[b] (UniformQuantizer.dequant, zp 0) */
+int fhe_dequantize(fhe_ctx* ctx, const int64_t* d_acc, int64_t B, double out_scale, double* d_score, void* stream);
+
+/* Top-k of d_acc over entries with d_below == 0 (or all if d_below is
+ * NULL), ordered by (acc desc, index asc) — Python's stable sort of
+ * batch_operations.py:282 on a monotone dequantisation. Indices are
+ * base_idx + position. Missing slots get acc = INT64_MIN, idx = -1. */
+int fhe_topk(fhe_ctx* ctx, const int64_t* d_acc, const int64_t* d_below, int64_t B, int64_t base_idx, int32_t k,
+             int64_t* d_out_acc, int64_t* d_out_idx, void* stream);
+
+/* ---- measurement ------------------------------------------------------------
+ * When enabled, every blind-rotation (external-product) and key-switch
+ * launch is bracketed by hipEvents on its own stream. fhe_profile_read
+ * synchronises and returns total milliseconds, launch count and ciphertexts
+ * processed for kernel "blind_rotate" or "keyswitch", then resets them. */
+int fhe_profile_enable(fhe_ctx* ctx, int enable);
+int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FHE_ICP_H */

@@ -1,0 +1,459 @@
+/*
+ * ORACLE (test infrastructure only) — exact CPU restatement of the
+ * FHEICP-TFHE v1 scheme that the MI355X kernels implement.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker. It is plain C (gcc, optional
+ * OpenMP) and shares NO code with the product (fhe-icp_amd/csrc): every
+ * primitive is written again from the spec in DESIGN.md §3.
+ *
+ * Reference anchor. The reference's encrypted path is
+ * FHESimilarityModel.predict_encrypted -> model.predict(X[i:i+1], fhe="execute")
+ * (fhe_similarity.py:142-160, :151): quantize -> encrypt -> leveled dot
+ * product with clear weights -> decrypt, run by concrete-python 2.10.0's CPU
+ * runtime (pinned at requirements.txt:5-7). That runtime is not in
+ * /root/reference and cannot be installed offline, so the TFHE parameters are
+ * this build's own; parity with the reference is asserted on the DECRYPTED
+ * integer accumulator, which tests compare with oracle/quant_ref.py (the
+ * restated Concrete-ML clear inference). The PBS stage (LSB-first bit
+ * extraction) has no reference counterpart; its parity
+ * target is the exact accumulator and the threshold bit of
+ * batch_operations.py:278.
+ *
+ * Arithmetic. Everything is exact integer arithmetic modulo 2^64 (unsigned
+ * wrap-around). Negacyclic polynomial products use Karatsuba over Z_{2^64},
+ * an exact ring algorithm, whereas the GPU uses an f64 FFT whose rounding is
+ * extra noise; so GPU and oracle agree bit-for-bit on keys, encryptions,
+ * linear combinations and key switching, agree on decrypted values after a
+ * bootstrap, and differ there only by a small bounded phase error
+ * (tests/test_gpu_parity.py checks both).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  int32_t n;               /* small LWE dimension */
+  int32_t k;               /* GLWE dimension */
+  int32_t N;               /* polynomial size (power of two) */
+  int32_t pbs_base_log;
+  int32_t pbs_level;
+  int32_t ks_base_log;
+  int32_t ks_level;
+  int32_t lwe_noise_bits;  /* TUniform bound: small LWE / KSK */
+  int32_t glwe_noise_bits; /* TUniform bound: GLWE / BSK / big-key LWE */
+  int32_t msg_bits;        /* P: message width */
+} ref_params;
+
+/* --------------------------------------------------------------- chacha --- */
+#define ROTL(a, b) (((a) << (b)) | ((a) >> (32 - (b))))
+#define QR(a, b, c, d) \
+  a += b; d ^= a; d = ROTL(d, 16); c += d; b ^= c; b = ROTL(b, 12); \
+  a += b; d ^= a; d = ROTL(d, 8);  c += d; b ^= c; b = ROTL(b, 7);
+
+typedef struct { uint32_t key[8]; } ref_key;
+
+/* RFC 8439 ChaCha20 block: state = consts | key | counter | nonce[3] */
+static void chacha20_block(const ref_key* K, uint32_t counter, uint32_t n0, uint32_t n1, uint32_t n2,
+                           uint32_t out[16]) {
+  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                    K->key[0], K->key[1], K->key[2], K->key[3], K->key[4], K->key[5], K->key[6], K->key[7],
+                    counter, n0, n1, n2};
+  uint32_t x[16];
+  memcpy(x, s, sizeof x);
+  for (int i = 0; i < 10; ++i) {
+    QR(x[0], x[4], x[8], x[12]); QR(x[1], x[5], x[9], x[13]);
+    QR(x[2], x[6], x[10], x[14]); QR(x[3], x[7], x[11], x[15]);
+    QR(x[0], x[5], x[10], x[15]); QR(x[1], x[6], x[11], x[12]);
+    QR(x[2], x[7], x[8], x[13]); QR(x[3], x[4], x[9], x[14]);
+  }
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+/* exposed for tests (RFC 8439 §2.3.2 vector) */
+void ref_chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]) {
+  ref_key K;
+  memcpy(K.key, key, 32);
+  chacha20_block(&K, counter, nonce[0], nonce[1], nonce[2], out);
+}
+
+/* Stream (tag, id): u64 word w = block w/8 (counter), words 2j, 2j+1 of it. */
+typedef struct {
+  const ref_key* K;
+  uint32_t tag;
+  uint64_t id;
+  uint64_t cur_block;
+  uint32_t buf[16];
+} ref_stream;
+
+static void stream_init(ref_stream* st, const ref_key* K, uint32_t tag, uint64_t id) {
+  st->K = K; st->tag = tag; st->id = id; st->cur_block = (uint64_t)-1;
+}
+static uint64_t stream_word(ref_stream* st, uint64_t w) {
+  uint64_t blk = w >> 3;
+  if (blk != st->cur_block) {
+    chacha20_block(st->K, (uint32_t)blk, st->tag, (uint32_t)st->id, (uint32_t)(st->id >> 32), st->buf);
+    st->cur_block = blk;
+  }
+  unsigned j = (unsigned)(w & 7);
+  return (uint64_t)st->buf[2 * j] | ((uint64_t)st->buf[2 * j + 1] << 32);
+}
+
+static uint64_t splitmix64(uint64_t* x) {
+  uint64_t z = (*x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static void key_from_seed(uint64_t seed, ref_key* K) {
+  uint64_t x = seed;
+  for (int i = 0; i < 4; ++i) {
+    uint64_t v = splitmix64(&x);
+    K->key[2 * i] = (uint32_t)v;
+    K->key[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+}
+
+/* TUniform(b) from one u64 word: b+2 low bits -> (bits>>1)+(bits&1) - 2^b */
+static int64_t tuniform(uint64_t w, int b) {
+  uint64_t bits = w & ((2ull << (b + 1)) - 1);
+  return (int64_t)((bits >> 1) + (bits & 1)) - ((int64_t)1 << b);
+}
+int64_t ref_tuniform(uint64_t w, int b) { return tuniform(w, b); }
+
+enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, TAG_KSK_MASK = 5,
+       TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8 };
+
+/* --------------------------------------------------- negacyclic product --- */
+/* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
+static void kara(const uint64_t* a, const uint64_t* b, uint64_t* c, int n, uint64_t* scratch) {
+  if (n <= 32) {
+    for (int i = 0; i < 2 * n - 1; ++i) c[i] = 0;
+    for (int i = 0; i < n; ++i) {
+      const uint64_t ai = a[i];
+      for (int j = 0; j < n; ++j) c[i + j] += ai * b[j];
+    }
+    return;
+  }
+  const int h = n / 2;
+  uint64_t* as = scratch;        /* h */
+  uint64_t* bs = scratch + h;    /* h */
+  uint64_t* mid = scratch + 2 * h; /* 2h-1 */
+  uint64_t* rest = scratch + 4 * h;
+  /* low and high products straight into c */
+  kara(a, b, c, h, rest);                 /* c[0..2h-2] */
+  c[2 * h - 1] = 0;
+  kara(a + h, b + h, c + 2 * h, h, rest); /* c[2h..4h-2] */
+  for (int i = 0; i < h; ++i) { as[i] = a[i] + a[i + h]; bs[i] = b[i] + b[i + h]; }
+  kara(as, bs, mid, h, rest);
+  for (int i = 0; i < 2 * h - 1; ++i) mid[i] -= c[i] + c[2 * h + i];
+  for (int i = 0; i < 2 * h - 1; ++i) c[h + i] += mid[i];
+}
+/* acc += a * b mod (X^N + 1), all mod 2^64. scratch >= 8N words */
+static void negacyclic_mac(const uint64_t* a, const uint64_t* b, uint64_t* acc, int N, uint64_t* scratch) {
+  uint64_t* full = scratch;          /* 2N */
+  kara(a, b, full, N, scratch + 2 * N);
+  full[2 * N - 1] = 0;
+  for (int t = 0; t < N; ++t) acc[t] += full[t] - full[t + N];
+}
+/* exposed for tests */
+void ref_negacyclic_mul(const uint64_t* a, const uint64_t* b, uint64_t* c, int N) {
+  uint64_t* scratch = (uint64_t*)malloc(8 * (size_t)(16 * N));
+  for (int t = 0; t < N; ++t) c[t] = 0;
+  negacyclic_mac(a, b, c, N, scratch);
+  free(scratch);
+}
+
+/* ---------------------------------------------------------------- sizes --- */
+static int rows(const ref_params* P) { return (P->k + 1) * P->pbs_level; }
+size_t ref_bsk_words(const ref_params* P) { return (size_t)P->n * rows(P) * (P->k + 1) * P->N; }
+size_t ref_ksk_words(const ref_params* P) { return (size_t)P->k * P->N * P->ks_level * (P->n + 1); }
+
+/* --------------------------------------------------------------- keygen --- */
+/* s_small[n] (0/1), s_big[kN] (0/1), bsk[ref_bsk_words], ksk[ref_ksk_words] */
+int ref_keygen(const ref_params* P, uint64_t seed, uint64_t* s_small, uint64_t* s_big, uint64_t* bsk,
+               uint64_t* ksk) {
+  ref_key K;
+  key_from_seed(seed, &K);
+  const int n = P->n, k = P->k, N = P->N, L = P->pbs_level, R = rows(P);
+  ref_stream st;
+  stream_init(&st, &K, TAG_SK_SMALL, 0);
+  for (int i = 0; i < n; ++i) s_small[i] = stream_word(&st, (uint64_t)i) & 1;
+  stream_init(&st, &K, TAG_SK_GLWE, 0);
+  for (int i = 0; i < k * N; ++i) s_big[i] = stream_word(&st, (uint64_t)i) & 1;
+
+  /* BSK rows: GLWE_S(0) + s_small[i] * g_lvl on component c_in, g_lvl = 2^(64 - lvl*beta) */
+#pragma omp parallel for schedule(dynamic)
+  for (int i = 0; i < n; ++i) {
+    uint64_t* scratch = (uint64_t*)malloc(8 * (size_t)(16 * N));
+    uint64_t* S = (uint64_t*)malloc(8 * (size_t)N);
+    ref_stream sm, sn;
+    for (int r = 0; r < R; ++r) {
+      const int c_in = r / L, lvl = r % L + 1;
+      uint64_t* row = bsk + ((size_t)i * R + r) * (k + 1) * N;
+      uint64_t* body = row + (size_t)k * N;
+      for (int t = 0; t < N; ++t) body[t] = 0;
+      for (int j = 0; j < k; ++j) {
+        uint64_t* A = row + (size_t)j * N;
+        stream_init(&sm, &K, TAG_BSK_MASK, ((uint64_t)i * R + r) * k + j);
+        for (int t = 0; t < N; ++t) A[t] = stream_word(&sm, (uint64_t)t);
+        for (int t = 0; t < N; ++t) S[t] = s_big[j * N + t];
+        negacyclic_mac(A, S, body, N, scratch);
+      }
+      stream_init(&sn, &K, TAG_BSK_NOISE, (uint64_t)i * R + r);
+      for (int t = 0; t < N; ++t) body[t] += (uint64_t)tuniform(stream_word(&sn, (uint64_t)t), P->glwe_noise_bits);
+      if (s_small[i]) row[(size_t)c_in * N] += ((uint64_t)1) << (64 - lvl * P->pbs_base_log);
+    }
+    free(scratch);
+    free(S);
+  }
+
+  /* key-switching key big -> small */
+  const int KL = P->ks_level;
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < k * N; ++i) {
+    ref_stream sm, sn;
+    for (int l = 0; l < KL; ++l) {
+      uint64_t* row = ksk + ((size_t)i * KL + l) * (n + 1);
+      stream_init(&sm, &K, TAG_KSK_MASK, (uint64_t)i * KL + l);
+      stream_init(&sn, &K, TAG_KSK_NOISE, (uint64_t)i * KL + l);
+      uint64_t b = 0;
+      for (int t = 0; t < n; ++t) {
+        row[t] = stream_word(&sm, (uint64_t)t);
+        if (s_small[t]) b += row[t];
+      }
+      b += (uint64_t)tuniform(stream_word(&sn, 0), P->lwe_noise_bits);
+      if (s_big[i]) b += ((uint64_t)1) << (64 - (l + 1) * P->ks_base_log);
+      row[n] = b;
+    }
+  }
+  return 0;
+}
+
+/* -------------------------------------------------------------- encrypt --- */
+/* Encrypt count torus messages msg[c] under s_big (dim kN); ciphertext ids
+ * are id0 + c. ct: count x (kN+1) words, layout [a_0..a_{kN-1}, b]. */
+void ref_encrypt_raw(const ref_params* P, const uint64_t* s_big, const uint64_t* msg, int64_t count,
+                     uint64_t seed, uint64_t id0, uint64_t* ct) {
+  ref_key K;
+  key_from_seed(seed, &K);
+  const int dim = P->k * P->N;
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < count; ++c) {
+    ref_stream sm, sn;
+    stream_init(&sm, &K, TAG_ENC_MASK, id0 + (uint64_t)c);
+    stream_init(&sn, &K, TAG_ENC_NOISE, id0 + (uint64_t)c);
+    uint64_t* o = ct + (size_t)c * (dim + 1);
+    uint64_t b = 0;
+    for (int t = 0; t < dim; ++t) {
+      o[t] = stream_word(&sm, (uint64_t)t);
+      if (s_big[t]) b += o[t];
+    }
+    b += (uint64_t)tuniform(stream_word(&sn, 0), P->glwe_noise_bits);
+    o[dim] = b + msg[c];
+  }
+}
+
+/* Encode signed integers v at Delta = 2^(64-P) and encrypt. */
+void ref_encrypt_ints(const ref_params* P, const uint64_t* s_big, const int64_t* v, int64_t count, uint64_t seed,
+                      uint64_t id0, uint64_t* ct) {
+  uint64_t* m = (uint64_t*)malloc(8 * (size_t)(count > 0 ? count : 1));
+  for (int64_t i = 0; i < count; ++i) m[i] = ((uint64_t)v[i]) << (64 - P->msg_bits);
+  ref_encrypt_raw(P, s_big, m, count, seed, id0, ct);
+  free(m);
+}
+
+static uint64_t lwe_phase(const uint64_t* ct, const uint64_t* s, int dim) {
+  uint64_t acc = ct[dim];
+  for (int t = 0; t < dim; ++t)
+    if (s[t]) acc -= ct[t];
+  return acc;
+}
+void ref_phase(const uint64_t* ct, const uint64_t* s, int dim, int64_t count, uint64_t* out) {
+  for (int64_t c = 0; c < count; ++c) out[c] = lwe_phase(ct + (size_t)c * (dim + 1), s, dim);
+}
+/* round(phase / 2^(64-P)) as a signed P-bit integer */
+static int64_t decode(uint64_t ph, int Pb) {
+  uint64_t r = ((ph >> (63 - Pb)) + 1) >> 1;
+  r &= (Pb >= 64) ? ~0ull : ((1ull << Pb) - 1);
+  if (r >> (Pb - 1)) return (int64_t)r - ((int64_t)1 << Pb);
+  return (int64_t)r;
+}
+void ref_decrypt_ints(const ref_params* P, const uint64_t* s_big, const uint64_t* ct, int64_t count, int64_t* out) {
+  const int dim = P->k * P->N;
+  for (int64_t c = 0; c < count; ++c) out[c] = decode(lwe_phase(ct + (size_t)c * (dim + 1), s_big, dim), P->msg_bits);
+}
+
+/* --------------------------------------------------------------- linear --- */
+/* out[b] = sum_j w[j] * ct[b, j] + trivial(cst * Delta); cts of dim kN. */
+void ref_linear(const ref_params* P, const uint64_t* ct, int64_t B, int32_t D, const int64_t* w, int64_t cst,
+                uint64_t* out) {
+  const int W = P->k * P->N + 1;
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < B; ++b) {
+    uint64_t* o = out + (size_t)b * W;
+    for (int t = 0; t < W; ++t) o[t] = 0;
+    for (int j = 0; j < D; ++j) {
+      const uint64_t* x = ct + ((size_t)b * D + j) * W;
+      const uint64_t wj = (uint64_t)w[j];
+      for (int t = 0; t < W; ++t) o[t] += wj * x[t];
+    }
+    o[W - 1] += ((uint64_t)cst) << (64 - P->msg_bits);
+  }
+}
+
+/* ------------------------------------------------------------ keyswitch --- */
+/* closest multiple of 2^(64 - L*bl), as L balanced digits d[0..L-1] (level 1 first) */
+static void decompose(uint64_t x, int bl, int L, int64_t* d) {
+  const int prec = L * bl;
+  uint64_t r = ((x >> (63 - prec)) + 1) >> 1;
+  r &= (prec >= 64) ? ~0ull : ((1ull << prec) - 1);
+  int64_t v = (int64_t)r;
+  const int64_t B = (int64_t)1 << bl;
+  for (int l = L; l >= 1; --l) {
+    int64_t dd = v & (B - 1);
+    v >>= bl;
+    if (dd >= B / 2) { dd -= B; v += 1; }
+    d[l - 1] = dd;
+  }
+}
+void ref_decompose(uint64_t x, int bl, int L, int64_t* d) { decompose(x, bl, L, d); }
+
+static void keyswitch1(const ref_params* P, const uint64_t* ksk, const uint64_t* in, uint64_t* out) {
+  const int n = P->n, dimb = P->k * P->N, KL = P->ks_level;
+  int64_t d[64];
+  for (int t = 0; t < n; ++t) out[t] = 0;
+  out[n] = in[dimb];
+  for (int i = 0; i < dimb; ++i) {
+    decompose(in[i], P->ks_base_log, KL, d);
+    for (int l = 0; l < KL; ++l) {
+      if (!d[l]) continue;
+      const uint64_t* row = ksk + ((size_t)i * KL + l) * (n + 1);
+      const uint64_t dd = (uint64_t)d[l];
+      for (int t = 0; t <= n; ++t) out[t] -= dd * row[t];
+    }
+  }
+}
+void ref_keyswitch(const ref_params* P, const uint64_t* ksk, const uint64_t* in, int64_t count, uint64_t* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < count; ++c)
+    keyswitch1(P, ksk, in + (size_t)c * (P->k * P->N + 1), out + (size_t)c * (P->n + 1));
+}
+
+/* ------------------------------------------------------- blind rotation --- */
+static int ilog2(int x) { int r = 0; while ((1 << r) < x) r++; return r; }
+/* round(a * 2N / 2^64) mod 2N */
+static uint32_t modswitch(uint64_t a, int log2N2) {
+  return (uint32_t)((((a >> (63 - log2N2)) + 1) >> 1) & ((1ull << log2N2) - 1));
+}
+
+/* Bootstrap one small LWE (dim n) with the constant test vector tv; sample
+ * extract coefficient 0. out: kN + 1 words under s_big. */
+static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small, uint64_t tv, uint64_t* out,
+                 uint64_t* work) {
+  const int n = P->n, k = P->k, N = P->N, L = P->pbs_level, R = rows(P), bl = P->pbs_base_log;
+  const int lg = ilog2(2 * N);
+  uint64_t* acc = work;                           /* (k+1)N */
+  uint64_t* dig = acc + (size_t)(k + 1) * N;      /* R*N */
+  uint64_t* scratch = dig + (size_t)R * N;        /* 16N */
+  int64_t d[64];
+  const uint32_t bt = modswitch(small[n], lg);
+  for (int t = 0; t < k * N; ++t) acc[t] = 0;
+  for (int t = 0; t < N; ++t) {
+    const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
+    acc[(size_t)k * N + t] = idx < (uint32_t)N ? tv : (uint64_t)0 - tv;
+  }
+  for (int i = 0; i < n; ++i) {
+    const uint32_t ai = modswitch(small[i], lg);
+    if (ai == 0) continue;
+    /* digits of X^{a_i} ACC - ACC */
+    for (int c = 0; c <= k; ++c) {
+      const uint64_t* f = acc + (size_t)c * N;
+      for (int t = 0; t < N; ++t) {
+        const uint32_t idx = (uint32_t)(t - (int)ai) & (2 * N - 1);
+        const uint64_t rot = idx < (uint32_t)N ? f[idx] : (uint64_t)0 - f[idx - N];
+        decompose(rot - f[t], bl, L, d);
+        for (int l = 0; l < L; ++l) dig[((size_t)c * L + l) * N + t] = (uint64_t)d[l];
+      }
+    }
+    /* ACC += sum_r dig_r * BSK_i[r] */
+    const uint64_t* G = bsk + (size_t)i * R * (k + 1) * N;
+    for (int r = 0; r < R; ++r)
+      for (int o = 0; o <= k; ++o)
+        negacyclic_mac(dig + (size_t)r * N, G + ((size_t)r * (k + 1) + o) * N, acc + (size_t)o * N, N, scratch);
+  }
+  for (int j = 0; j < k; ++j) {
+    const uint64_t* A = acc + (size_t)j * N;
+    out[(size_t)j * N] = A[0];
+    for (int t = 1; t < N; ++t) out[(size_t)j * N + t] = (uint64_t)0 - A[N - t];
+  }
+  out[(size_t)k * N] = acc[(size_t)k * N];
+}
+static size_t pbs_work_words(const ref_params* P) {
+  return (size_t)(P->k + 1) * P->N + (size_t)rows(P) * P->N + 16 * (size_t)P->N;
+}
+
+/* Bootstrap count small LWEs with a constant test vector (amplitude tv). */
+void ref_pbs_const(const ref_params* P, const uint64_t* bsk, const uint64_t* small, int64_t count, uint64_t tv,
+                   uint64_t* out) {
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c)
+      pbs1(P, bsk, small + (size_t)c * (P->n + 1), tv, out + (size_t)c * (P->k * P->N + 1), work);
+    free(work);
+  }
+}
+
+/* modswitched (a~, b~) of small LWEs, for tests */
+void ref_modswitch(const ref_params* P, const uint64_t* small, int64_t count, uint32_t* out) {
+  const int lg = ilog2(2 * P->N);
+  for (int64_t c = 0; c < count * (P->n + 1); ++c) out[c] = modswitch(small[c], lg);
+}
+
+/* ------------------------------------------------------- bit extraction --- */
+/* LSB-first extraction of the P bits of v from ct_v (encrypting v * 2^(64-P)),
+ * DESIGN.md §3.4. Iteration i: sh = ct_v * 2^(P-1-i) (+2^62 on the body),
+ * KS, PBS with constant tv = 2^(63-P+i), bit_i = trivial(tv) - PBS (encrypts
+ * bit_i * 2^(64-P+i)), ct_v -= bit_i, refreshed += bit_i.
+ * refreshed[count x (kN+1)] encrypts v; sign[count x (kN+1)] is bit P-1.
+ * ct_v is consumed (overwritten). */
+void ref_bit_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
+                     uint64_t* refreshed, uint64_t* sign) {
+  const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+    uint64_t* sh = (uint64_t*)malloc(8 * (size_t)Wb);
+    uint64_t* sm = (uint64_t*)malloc(8 * (size_t)(P->n + 1));
+    uint64_t* ob = (uint64_t*)malloc(8 * (size_t)Wb);
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c) {
+      uint64_t* cv = ct_v + (size_t)c * Wb;
+      uint64_t* acc = refreshed + (size_t)c * Wb;
+      for (int t = 0; t < Wb; ++t) acc[t] = 0;
+      for (int i = 0; i < Pb; ++i) {
+        const int s = Pb - 1 - i;
+        for (int t = 0; t < Wb; ++t) sh[t] = cv[t] << s;
+        sh[Wb - 1] += 1ull << 62;
+        keyswitch1(P, ksk, sh, sm);
+        const uint64_t tv = 1ull << (63 - Pb + i);
+        pbs1(P, bsk, sm, tv, ob, work);
+        for (int t = 0; t < Wb - 1; ++t) ob[t] = (uint64_t)0 - ob[t];
+        ob[Wb - 1] = tv - ob[Wb - 1];
+        for (int t = 0; t < Wb; ++t) { cv[t] -= ob[t]; acc[t] += ob[t]; }
+        if (i == Pb - 1) memcpy(sign + (size_t)c * Wb, ob, 8 * (size_t)Wb);
+      }
+    }
+    free(work); free(sh); free(sm); free(ob);
+  }
+}
+
+/* Decrypt the sign ciphertext: 1 iff phase in [2^62, 3*2^62) i.e. bit set. */
+void ref_decrypt_bits(const ref_params* P, const uint64_t* s_big, const uint64_t* ct, int64_t count, int64_t* out) {
+  const int dim = P->k * P->N;
+  for (int64_t c = 0; c < count; ++c) {
+    uint64_t ph = lwe_phase(ct + (size_t)c * (dim + 1), s_big, dim);
+    out[c] = (int64_t)(((ph + (1ull << 62)) >> 63) & 1);
+  }
+}

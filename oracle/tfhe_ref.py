@@ -1,0 +1,197 @@
+"""ORACLE (test infrastructure only) — ctypes binding of oracle/build/libtfhe_ref.so.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this, and only as the checker. See oracle/tfhe_ref.c for what it restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "build" / "libtfhe_ref.so"
+
+FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
+          "lwe_noise_bits", "glwe_noise_bits", "msg_bits")
+
+
+class RefParams(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in FIELDS]
+
+
+def build() -> Path:
+    """Compile the oracle with make (gcc). Output only under oracle/build/."""
+    subprocess.run(["make", "-s", "-C", str(_HERE)], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(_LIB_PATH))
+        P = C.POINTER(RefParams)
+        u64p = C.POINTER(C.c_uint64)
+        i64p = C.POINTER(C.c_int64)
+        u32p = C.POINTER(C.c_uint32)
+        L.ref_bsk_words.argtypes = [P]; L.ref_bsk_words.restype = C.c_size_t
+        L.ref_ksk_words.argtypes = [P]; L.ref_ksk_words.restype = C.c_size_t
+        L.ref_keygen.argtypes = [P, C.c_uint64, u64p, u64p, u64p, u64p]
+        L.ref_encrypt_raw.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, u64p]
+        L.ref_encrypt_ints.argtypes = [P, u64p, i64p, C.c_int64, C.c_uint64, C.c_uint64, u64p]
+        L.ref_phase.argtypes = [u64p, u64p, C.c_int, C.c_int64, u64p]
+        L.ref_decrypt_ints.argtypes = [P, u64p, u64p, C.c_int64, i64p]
+        L.ref_decrypt_bits.argtypes = [P, u64p, u64p, C.c_int64, i64p]
+        L.ref_linear.argtypes = [P, u64p, C.c_int64, C.c_int32, i64p, C.c_int64, u64p]
+        L.ref_keyswitch.argtypes = [P, u64p, u64p, C.c_int64, u64p]
+        L.ref_modswitch.argtypes = [P, u64p, C.c_int64, u32p]
+        L.ref_pbs_const.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, u64p]
+        L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
+        L.ref_negacyclic_mul.argtypes = [u64p, u64p, u64p, C.c_int]
+        L.ref_decompose.argtypes = [C.c_uint64, C.c_int, C.c_int, i64p]
+        L.ref_tuniform.argtypes = [C.c_uint64, C.c_int]; L.ref_tuniform.restype = C.c_int64
+        L.ref_chacha20_block.argtypes = [u32p, C.c_uint32, u32p, u32p]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, ct):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def u64(a):
+    return _p(a, C.c_uint64)
+
+
+def i64(a):
+    return _p(a, C.c_int64)
+
+
+class RefTFHE:
+    """Exact CPU TFHE with the same parameters and PRNG streams as the GPU."""
+
+    def __init__(self, params: dict, seed: int):
+        self.params = {f: int(params[f]) for f in FIELDS}
+        self.P = RefParams(**self.params)
+        L = lib()
+        self.n, self.k, self.N = self.params["n"], self.params["k"], self.params["N"]
+        self.big = self.k * self.N
+        self.s_small = np.zeros(self.n, np.uint64)
+        self.s_big = np.zeros(self.big, np.uint64)
+        self.bsk = np.zeros(L.ref_bsk_words(C.byref(self.P)), np.uint64)
+        self.ksk = np.zeros(L.ref_ksk_words(C.byref(self.P)), np.uint64)
+        L.ref_keygen(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big), u64(self.bsk),
+                     u64(self.ksk))
+
+    def with_msg_bits(self, P: int) -> "RefTFHE":
+        self.params["msg_bits"] = int(P)
+        self.P = RefParams(**self.params)
+        return self
+
+    def encrypt_ints(self, v, seed: int, id0: int = 0) -> np.ndarray:
+        v = np.ascontiguousarray(v, dtype=np.int64).reshape(-1)
+        ct = np.zeros((v.size, self.big + 1), np.uint64)
+        lib().ref_encrypt_ints(C.byref(self.P), u64(self.s_big), i64(v), v.size, seed, id0, u64(ct))
+        return ct
+
+    def encrypt_raw(self, msg, seed: int, id0: int = 0) -> np.ndarray:
+        msg = np.ascontiguousarray(msg, dtype=np.uint64).reshape(-1)
+        ct = np.zeros((msg.size, self.big + 1), np.uint64)
+        lib().ref_encrypt_raw(C.byref(self.P), u64(self.s_big), u64(msg), msg.size, seed, id0, u64(ct))
+        return ct
+
+    def phase(self, ct: np.ndarray, small: bool = False) -> np.ndarray:
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        s = self.s_small if small else self.s_big
+        dim = s.size
+        cnt = ct.size // (dim + 1)
+        out = np.zeros(cnt, np.uint64)
+        lib().ref_phase(u64(ct), u64(s), dim, cnt, u64(out))
+        return out
+
+    def decrypt_ints(self, ct: np.ndarray) -> np.ndarray:
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        cnt = ct.size // (self.big + 1)
+        out = np.zeros(cnt, np.int64)
+        lib().ref_decrypt_ints(C.byref(self.P), u64(self.s_big), u64(ct), cnt, i64(out))
+        return out
+
+    def decrypt_bits(self, ct: np.ndarray) -> np.ndarray:
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        cnt = ct.size // (self.big + 1)
+        out = np.zeros(cnt, np.int64)
+        lib().ref_decrypt_bits(C.byref(self.P), u64(self.s_big), u64(ct), cnt, i64(out))
+        return out
+
+    def linear(self, ct: np.ndarray, B: int, D: int, w, cst: int) -> np.ndarray:
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        w = np.ascontiguousarray(w, dtype=np.int64)
+        out = np.zeros((B, self.big + 1), np.uint64)
+        lib().ref_linear(C.byref(self.P), u64(ct), B, D, i64(w), cst, u64(out))
+        return out
+
+    def keyswitch(self, ct: np.ndarray) -> np.ndarray:
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        cnt = ct.size // (self.big + 1)
+        out = np.zeros((cnt, self.n + 1), np.uint64)
+        lib().ref_keyswitch(C.byref(self.P), u64(self.ksk), u64(ct), cnt, u64(out))
+        return out
+
+    def modswitch(self, small: np.ndarray) -> np.ndarray:
+        small = np.ascontiguousarray(small, dtype=np.uint64)
+        cnt = small.size // (self.n + 1)
+        out = np.zeros((cnt, self.n + 1), np.uint32)
+        lib().ref_modswitch(C.byref(self.P), u64(small), cnt, _p(out, C.c_uint32))
+        return out
+
+    def pbs_const(self, small: np.ndarray, tv: int) -> np.ndarray:
+        small = np.ascontiguousarray(small, dtype=np.uint64)
+        cnt = small.size // (self.n + 1)
+        out = np.zeros((cnt, self.big + 1), np.uint64)
+        lib().ref_pbs_const(C.byref(self.P), u64(self.bsk), u64(small), cnt, C.c_uint64(tv), u64(out))
+        return out
+
+    def bit_extract(self, ct_v: np.ndarray):
+        cv = np.array(ct_v, dtype=np.uint64, copy=True, order="C")
+        cnt = cv.size // (self.big + 1)
+        ref = np.zeros((cnt, self.big + 1), np.uint64)
+        sign = np.zeros((cnt, self.big + 1), np.uint64)
+        lib().ref_bit_extract(C.byref(self.P), u64(self.bsk), u64(self.ksk), u64(cv), cnt, u64(ref), u64(sign))
+        return ref, sign
+
+
+def negacyclic_mul(a, b) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    c = np.zeros_like(a)
+    lib().ref_negacyclic_mul(u64(a), u64(b), u64(c), a.size)
+    return c
+
+
+def decompose(x: int, base_log: int, levels: int) -> np.ndarray:
+    d = np.zeros(levels, np.int64)
+    lib().ref_decompose(C.c_uint64(x), base_log, levels, i64(d))
+    return d
+
+
+def tuniform(w: int, b: int) -> int:
+    return int(lib().ref_tuniform(C.c_uint64(w), b))
+
+
+def chacha20_block(key_words, counter: int, nonce_words) -> np.ndarray:
+    k = np.ascontiguousarray(key_words, dtype=np.uint32)
+    n = np.ascontiguousarray(nonce_words, dtype=np.uint32)
+    out = np.zeros(16, np.uint32)
+    lib().ref_chacha20_block(_p(k, C.c_uint32), counter, _p(n, C.c_uint32), _p(out, C.c_uint32))
+    return out
+
+

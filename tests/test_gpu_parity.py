@@ -1,0 +1,174 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the exact CPU oracle.
+
+Bit-exact: key material, encryptions, linear combinations, key switching,
+and every decrypted value. After a bootstrap the GPU's f64-FFT rounding
+differs from the oracle's exact Karatsuba product by a bounded phase error,
+checked against a tolerance well inside the decision margin.
+"""
+import numpy as np
+import pytest
+import torch
+
+from fheicp.params import TOY, SchemeParams, params_for_bits
+from fheicp.engine import Engine, u64
+
+pytestmark = pytest.mark.gpu
+
+REAL16 = params_for_bits(16)
+
+
+def signed(x):
+    return np.asarray(x, dtype=np.uint64).view(np.int64)
+
+
+@pytest.fixture(scope="module")
+def toy(need_gpu, oracle_lib):
+    eng = Engine(TOY, 0)
+    eng.keygen(1234)
+    ref = oracle_lib.RefTFHE(TOY.as_dict(), 1234)
+    return eng, ref
+
+
+@pytest.fixture(scope="module")
+def real(need_gpu, oracle_lib):
+    eng = Engine(REAL16, 0)
+    eng.keygen(777)
+    ref = oracle_lib.RefTFHE(REAL16.as_dict(), 777)
+    return eng, ref
+
+
+@pytest.mark.parametrize("which", ["toy", "real"])
+def test_keygen_bit_exact(which, request):
+    eng, ref = request.getfixturevalue(which)
+    keys = eng.export_keys()
+    assert np.array_equal(keys["s_small"], ref.s_small)
+    assert np.array_equal(keys["s_big"], ref.s_big)
+    assert np.array_equal(keys["ksk"], ref.ksk)
+    assert np.array_equal(keys["bsk"], ref.bsk)
+
+
+@pytest.mark.parametrize("which", ["toy", "real"])
+def test_encrypt_decrypt_bit_exact(which, request):
+    eng, ref = request.getfixturevalue(which)
+    P = eng.msg_bits
+    rng = np.random.default_rng(5)
+    v = rng.integers(-(2 ** (P - 1)), 2 ** (P - 1), 300)
+    v[:4] = [-(2 ** (P - 1)), 2 ** (P - 1) - 1, 0, -1]
+    ct = eng.encrypt(v, seed=99, id0=1000)
+    ct_ref = ref.encrypt_ints(v, seed=99, id0=1000)
+    assert np.array_equal(u64(ct).reshape(ct_ref.shape), ct_ref)
+    assert np.array_equal(eng.decrypt(ct).cpu().numpy(), v)
+    assert np.array_equal(ref.decrypt_ints(ct_ref), v)
+
+
+@pytest.mark.parametrize("which", ["toy", "real"])
+def test_linear_and_keyswitch_bit_exact(which, request):
+    eng, ref = request.getfixturevalue(which)
+    P = eng.msg_bits
+    rng = np.random.default_rng(6)
+    B, D = 40, 16
+    x = rng.integers(-8, 8, (B, D))
+    w = rng.integers(-31, 32, D)
+    cst = int(rng.integers(-100, 100))
+    ct = eng.encrypt(x, seed=3)
+    ct_ref = ref.encrypt_ints(x, seed=3)
+    lin = eng.linear(ct, B, D, w, cst)
+    lin_ref = ref.linear(ct_ref, B, D, w, cst)
+    assert np.array_equal(u64(lin), lin_ref)
+    half = 2 ** (P - 1)
+    expect = (x @ w + cst + half) % (2 * half) - half   # arithmetic mod 2^P
+    assert np.array_equal(eng.decrypt(lin).cpu().numpy(), expect)
+    for shift, add in ((0, 0), (P - 3, 1 << 62)):
+        ks = eng.keyswitch(lin, shift, add)
+        sh = (lin_ref << np.uint64(shift))
+        sh[:, -1] += np.uint64(add)
+        ks_ref = ref.keyswitch(sh)
+        assert np.array_equal(u64(ks), ks_ref), f"keyswitch shift={shift}"
+
+
+def test_pbs_matches_oracle_toy(toy):
+    eng, ref = toy
+    rng = np.random.default_rng(7)
+    v = rng.integers(-128, 128, 24)
+    ct = eng.encrypt(v, seed=11)
+    small = eng.keyswitch(ct, 0, 0)
+    tv = 1 << 61
+    out = eng.pbs(small, tv)
+    out_ref = ref.pbs_const(u64(small), tv)
+    ph = signed(u64(eng.phase(out)))
+    ph_ref = signed(ref.phase(out_ref))
+    # sign of the bootstrapped phase follows the input phase half-torus
+    expect = np.where(v >= 0, tv, -tv)
+    assert np.all(np.abs(ph - expect) < 2 ** 52)
+    assert np.all(np.abs(ph_ref - expect) < 2 ** 52)
+    # GPU f64 FFT vs exact product. Mask words diverge as soon as one gadget
+    # digit rounds the other way (a +-1 digit adds a whole random BSK row),
+    # but the phases must agree to within noise level.
+    assert np.abs(ph - ph_ref).max() < 2 ** 48
+
+
+def test_bit_extract_toy(toy):
+    eng, ref = toy
+    P = eng.msg_bits
+    rng = np.random.default_rng(8)
+    v = rng.integers(-(2 ** (P - 1)), 2 ** (P - 1), 64)
+    v[:3] = [-(2 ** (P - 1)), 2 ** (P - 1) - 1, 0]
+    ct = eng.encrypt(v, seed=12)
+    ref_ct, sign = eng.bit_extract(ct)
+    assert np.array_equal(eng.decrypt(ref_ct).cpu().numpy(), v)
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    # oracle on a few, bit-exact decrypts and close phases
+    ct_ref = ref.encrypt_ints(v[:4], seed=12)
+    r2, s2 = ref.bit_extract(ct_ref)
+    assert np.array_equal(ref.decrypt_ints(r2), v[:4])
+    d = signed(u64(eng.phase(ref_ct[:4].contiguous())) - ref.phase(r2))
+    assert np.abs(d).max() < 2 ** (64 - P - 4)
+
+
+def test_bit_extract_real_params(real):
+    eng, ref = real
+    P = eng.msg_bits
+    rng = np.random.default_rng(9)
+    v = rng.integers(-(2 ** (P - 1)), 2 ** (P - 1), 256)
+    v[:4] = [-(2 ** (P - 1)), 2 ** (P - 1) - 1, 0, -1]
+    ct = eng.encrypt(v, seed=21)
+    ref_ct, sign = eng.bit_extract(ct)
+    got = eng.decrypt(ref_ct).cpu().numpy()
+    assert np.array_equal(got, v)
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    # refreshed = sum of P bit ciphertexts: noise ~ sqrt(P) * sigma_pbs
+    # (DESIGN.md §3.5), still inside the Delta/2 decoding margin
+    ph = signed(u64(eng.phase(ref_ct)))
+    err = ph - (v.astype(np.int64) << (64 - P))
+    assert np.abs(err).max() < 2 ** (63 - P)
+    assert np.std(err.astype(np.float64)) < 2 ** 45.5
+
+
+def test_single_pbs_real_vs_oracle(real):
+    eng, ref = real
+    v = np.array([-30000, -12000, 12000, 30000], dtype=np.int64)  # |phase| >> KS+MS noise
+    ct = eng.encrypt(v, seed=31)
+    small = eng.keyswitch(ct, 0, 0)
+    out = eng.pbs(small, 1 << 62)
+    out_ref = ref.pbs_const(u64(small), 1 << 62)
+    ph = signed(u64(eng.phase(out)))
+    ph_ref = signed(ref.phase(out_ref))
+    assert np.abs(ph - ph_ref).max() < 2 ** 48
+    assert np.array_equal(ph > 0, v >= 0)
+
+
+def test_topk_matches_stable_sort(need_gpu):
+    eng = Engine(TOY, 0)
+    rng = np.random.default_rng(10)
+    for B, k in ((1000, 10), (37, 50), (5000, 1), (0, 3)):
+        acc = rng.integers(-20, 20, B)   # many ties
+        below = (rng.random(B) < 0.3).astype(np.int64)
+        oa, oi = eng.topk(eng.to_dev(acc), eng.to_dev(below), k, base_idx=100)
+        keep = [(i, int(acc[i])) for i in range(B) if not below[i]]
+        keep.sort(key=lambda x: x[1], reverse=True)     # Python stable sort
+        exp = keep[:k]
+        got_i = oi.cpu().numpy()
+        got_a = oa.cpu().numpy()
+        assert [int(i) - 100 for i in got_i[:len(exp)]] == [i for i, _ in exp]
+        assert [int(a) for a in got_a[:len(exp)]] == [a for _, a in exp]
+        assert np.all(got_i[len(exp):] == -1)
