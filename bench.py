@@ -105,6 +105,7 @@ def main():
     p = eng.params
     P = model.msg_bits
     from fheicp.model import threshold_int
+    from fheicp.search import sharded_topk
     T = threshold_int(model.qparams, args.min_similarity)
 
     q_np, docs_np = shard(args, rank)
@@ -116,18 +117,7 @@ def main():
     def step():
         qx = model.quantize_dev(d_dev, q_dev)
         acc, below = model.encrypted_acc(qx, T)
-        oa, oi = eng.topk(acc, below, args.top_k, base_idx)
-        if world > 1:
-            # the sharded search's one exchange: all-gather k (acc, idx) per rank
-            ga = [torch.empty_like(oa) for _ in range(world)]
-            gi = [torch.empty_like(oi) for _ in range(world)]
-            torch.distributed.all_gather(ga, oa)
-            torch.distributed.all_gather(gi, oi)
-            cat_a, cat_i = torch.cat(ga), torch.cat(gi)
-            # merge with the same (acc desc, idx asc) order: ranks own ascending
-            # contiguous index ranges, so position order == global index order
-            oa, pos = eng.topk(cat_a, (cat_i < 0).to(torch.int64), args.top_k, 0)
-            oi = torch.where(pos >= 0, cat_i[pos.clamp(min=0)], pos)
+        oa, oi = sharded_topk(acc, below, args.top_k, base_idx, eng.topk, world)
         return acc, below, oa, oi
 
     for _ in range(args.warmup):

@@ -34,12 +34,14 @@ def training_pairs(input_dim: int, n_samples: int = 1000, seed: int = 0, similar
 
 
 def corpus(input_dim: int, n_docs: int, seed: int, query_seed: int | None = None):
-    """(query f32 [D], docs f32 [n_docs, D]); the query comes from query_seed
-    (so every shard of a sharded corpus shares it), docs from seed."""
-    qrng = np.random.default_rng(seed if query_seed is None else query_seed)
+    """(query f32 [D], docs f32 [n_docs, D]). With query_seed=None the query
+    is the first draw of the seed's stream (one stream, as
+    oracle.quant_ref.make_corpus); otherwise it comes from its own stream so
+    every shard of a sharded corpus shares it while docs differ per seed."""
+    rng = np.random.default_rng(seed)
+    qrng = rng if query_seed is None else np.random.default_rng(query_seed)
     q = qrng.standard_normal(input_dim).astype(np.float32)
     q /= np.linalg.norm(q)
-    rng = np.random.default_rng(seed)
     docs = rng.standard_normal((n_docs, input_dim)).astype(np.float32)
     docs /= np.linalg.norm(docs, axis=1, keepdims=True)
     mask = rng.random(n_docs) > 0.5

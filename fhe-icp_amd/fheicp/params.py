@@ -38,14 +38,14 @@ class SchemeParams:
 
 
 # Bootstrap gadget by message width (checked by noise_report()).
-PBS_GADGETS = ((18, 15, 2), (22, 12, 3), (24, 10, 4), (26, 8, 5), (28, 7, 6))
+PBS_GADGETS = ((18, 15, 2), (22, 12, 3), (24, 10, 4), (26, 8, 5), (27, 7, 6))
 
 
 def params_for_bits(P: int) -> SchemeParams:
     for pmax, beta, lvl in PBS_GADGETS:
         if P <= pmax:
             return SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
-    raise ValueError(f"accumulator width P={P} exceeds the supported 28 bits")
+    raise ValueError(f"accumulator width P={P} exceeds the supported 27 bits")
 
 
 # A tiny, INSECURE set with the same structure, for fast functional tests.

@@ -1,0 +1,33 @@
+"""Sharded corpus search: per-shard top-k + one all-gather + merge.
+
+Replaces the sequential per-document loop of BatchProcessor.search_similar
+(batch_operations.py:268-284). Every rank owns a contiguous range of global
+document indices (index.json insertion order, encrypted_storage.py:136-141),
+computes encrypted compares and its local top-k by (acc desc, index asc) —
+the order Python's stable sort gives batch_operations.py:282 on a monotone
+dequantisation — and the ranks exchange k (acc, index) pairs with ONE
+all-gather (RCCL over xGMI on MI355X; gloo in the CPU tests). Because rank r's
+indices all precede rank r+1's, merging by (acc desc, position asc) over the
+rank-ordered concatenation is exactly (acc desc, global index asc).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def sharded_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx: int, topk_fn,
+                 world: int = 1, group=None):
+    """topk_fn(acc, below, k, base_idx) -> (acc_k, idx_k), missing slots idx -1.
+
+    Returns the global top-k (identical on every rank)."""
+    oa, oi = topk_fn(acc, below, k, base_idx)
+    if world == 1:
+        return oa, oi
+    ga = [torch.empty_like(oa) for _ in range(world)]
+    gi = [torch.empty_like(oi) for _ in range(world)]
+    torch.distributed.all_gather(ga, oa, group=group)
+    torch.distributed.all_gather(gi, oi, group=group)
+    cat_a, cat_i = torch.cat(ga), torch.cat(gi)
+    ma, pos = topk_fn(cat_a, (cat_i < 0).to(torch.int64), k, 0)
+    mi = torch.where(pos >= 0, cat_i[pos.clamp(min=0)], pos)
+    return ma, mi

@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library loads, exports every symbol include/fhe_icp.h
+declares, validates parameters and fails loudly without a device. No compute
+calls (there is no GPU here)."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import pytest
+
+from fheicp import _lib
+from fheicp.params import TOY, params_for_bits
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "fhe_icp.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fhe_[a-z_0-9]+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ("fhe_ctx_create", "fhe_keygen", "fhe_encrypt_batch", "fhe_linear_batch", "fhe_keyswitch_batch",
+                 "fhe_pbs_batch", "fhe_bit_extract_batch", "fhe_decrypt_batch", "fhe_compare_batch", "fhe_topk"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    # and the Python binding covers all of them
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(declared_functions()) <= bound
+
+
+def test_sizes_match_oracle(oracle_lib):
+    L = _lib.lib()
+    for p in (TOY, params_for_bits(16), params_for_bits(21), params_for_bits(26)):
+        P = _lib.params_struct(p.as_dict())
+        R = oracle_lib.RefParams(**p.as_dict())
+        ol = oracle_lib.lib()
+        assert L.fhe_bsk_words(C.byref(P)) == ol.ref_bsk_words(C.byref(R))
+        assert L.fhe_ksk_words(C.byref(P)) == ol.ref_ksk_words(C.byref(R))
+        assert L.fhe_big_lwe_words(C.byref(P)) == p.k * p.N + 1
+        assert L.fhe_small_lwe_words(C.byref(P)) == p.n + 1
+
+
+def test_host_context_and_validation():
+    L = _lib.lib()
+    P = _lib.params_struct(params_for_bits(16).as_dict())
+    h = C.c_void_p()
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0 and h.value
+    got = _lib.FheParams()
+    assert L.fhe_get_params(h, C.byref(got)) == 0 and got.n == 887 and got.msg_bits == 16
+    assert L.fhe_set_msg_bits(h, 60) == -1
+    assert b"msg_bits" in L.fhe_last_error(h)
+    # host-only contexts refuse device work with a clear error
+    assert L.fhe_keygen(h, 1, None) == -2
+    assert b"host-only" in L.fhe_last_error(h)
+    L.fhe_ctx_destroy(h)
+    bad = dict(params_for_bits(16).as_dict(), N=1000)
+    Pb = _lib.params_struct(bad)
+    assert L.fhe_ctx_create(C.byref(Pb), -1, C.byref(h)) == -1
+    assert b"N must be" in L.fhe_last_error(None)
+
+
+def test_engine_refuses_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from fheicp.engine import Engine
+    with pytest.raises(_lib.FheError):
+        Engine(TOY, 0)

@@ -1,0 +1,127 @@
+"""CPU: the exact TFHE oracle — primitives against published vectors and
+schoolbook math, the scheme end-to-end on the TOY set, and spec digests."""
+import hashlib
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from fheicp.params import TOY, params_for_bits
+
+GOLD = json.loads((Path(__file__).parent / "golden" / "tfhe_golden.json").read_text())
+
+
+def test_chacha20_rfc8439_block(oracle_lib):
+    """RFC 8439 §2.3.2 test vector."""
+    key = np.frombuffer(bytes(range(32)), dtype="<u4")
+    nonce = np.frombuffer(bytes.fromhex("000000090000004a00000000"), dtype="<u4")
+    out = oracle_lib.chacha20_block(key, 1, nonce)
+    expect = [0xe4e7f110, 0x15593bd1, 0x1fdd0f50, 0xc47120a3, 0xc7f4d1c7, 0x0368c033, 0x9aaa2204, 0x4e6cd4c3,
+              0x466482d2, 0x09aa9f07, 0x05d7c214, 0xa2028bd9, 0xd19c12b5, 0xb94e16de, 0xe883d0cb, 0x4e3c50a2]
+    assert out.tolist() == expect
+
+
+def test_tuniform_support(oracle_lib):
+    b = 5
+    vals = [oracle_lib.tuniform(w, b) for w in range(1 << (b + 2))]
+    assert min(vals) == -(1 << b) and max(vals) == (1 << b)
+    counts = np.bincount(np.array(vals) + (1 << b))
+    assert counts[0] == 1 and counts[-1] == 1 and set(counts[1:-1]) == {2}
+
+
+@pytest.mark.parametrize("N", [16, 64, 256])
+def test_negacyclic_karatsuba_vs_schoolbook(oracle_lib, N):
+    rng = np.random.default_rng(N)
+    a = rng.integers(0, 2 ** 63, N, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    b = rng.integers(0, 2 ** 63, N, dtype=np.uint64)
+    c = oracle_lib.negacyclic_mul(a, b)
+    ref = [0] * N
+    for i in range(N):
+        for j in range(N):
+            p = int(a[i]) * int(b[j])
+            if i + j < N:
+                ref[i + j] += p
+            else:
+                ref[i + j - N] -= p
+    assert c.tolist() == [x % 2 ** 64 for x in ref]
+
+
+@pytest.mark.parametrize("beta,levels", [(15, 2), (12, 3), (7, 6), (4, 4)])
+def test_gadget_decomposition(oracle_lib, beta, levels):
+    rng = np.random.default_rng(beta)
+    for x in list(rng.integers(0, 2 ** 64, 200, dtype=np.uint64)) + [0, 2 ** 64 - 1, 2 ** 63]:
+        d = oracle_lib.decompose(int(x), beta, levels)
+        assert np.all(d >= -(2 ** (beta - 1))) and np.all(d < 2 ** (beta - 1))
+        rec = sum(int(d[l]) << (64 - (l + 1) * beta) for l in range(levels)) % 2 ** 64
+        err = (int(x) - rec) % 2 ** 64
+        err = err - 2 ** 64 if err >= 2 ** 63 else err
+        assert abs(err) <= 2 ** (63 - levels * beta)
+
+
+@pytest.fixture(scope="module")
+def toy_ref(oracle_lib):
+    return oracle_lib.RefTFHE(TOY.as_dict(), GOLD["key_seed"])
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_spec_digests(toy_ref):
+    """Key streams and encryption streams are frozen by the spec."""
+    assert sha(toy_ref.s_small) == GOLD["sha256_s_small"]
+    assert sha(toy_ref.s_big) == GOLD["sha256_s_big"]
+    assert sha(toy_ref.bsk) == GOLD["sha256_bsk"]
+    assert sha(toy_ref.ksk) == GOLD["sha256_ksk"]
+    ct = toy_ref.encrypt_ints(np.array(GOLD["messages"]), seed=GOLD["enc_seed"], id0=GOLD["id0"])
+    assert sha(ct) == GOLD["sha256_ct"]
+
+
+def test_encrypt_linear_decrypt(toy_ref):
+    P = TOY.msg_bits
+    rng = np.random.default_rng(1)
+    x = rng.integers(-4, 4, (30, 8))
+    w = rng.integers(-7, 8, 8)
+    ct = toy_ref.encrypt_ints(x, seed=5)
+    assert np.array_equal(toy_ref.decrypt_ints(ct), x.reshape(-1))
+    lin = toy_ref.linear(ct, 30, 8, w, 3)
+    half = 2 ** (P - 1)
+    assert np.array_equal(toy_ref.decrypt_ints(lin), (x @ w + 3 + half) % (2 * half) - half)
+
+
+def test_keyswitch_noise(toy_ref):
+    rng = np.random.default_rng(2)
+    v = rng.integers(-100, 100, 40)
+    ct = toy_ref.encrypt_ints(v, seed=6)
+    sm = toy_ref.keyswitch(ct)
+    ph = toy_ref.phase(sm, small=True).view(np.int64)
+    err = ph - (v.astype(np.int64) << (64 - TOY.msg_bits))
+    assert np.abs(err).max() < 2 ** 58     # TOY n=64: sigma_ks ~ 2^-8 of the torus
+
+
+def test_pbs_sign_and_bit_extraction(toy_ref):
+    P = TOY.msg_bits
+    v = np.array([-(2 ** (P - 1)), -77, -1, 0, 1, 42, 2 ** (P - 1) - 1], dtype=np.int64)
+    ct = toy_ref.encrypt_ints(v, seed=7)
+    ref, sign = toy_ref.bit_extract(ct)
+    assert np.array_equal(toy_ref.decrypt_ints(ref), v)
+    assert np.array_equal(toy_ref.decrypt_bits(sign), (v < 0).astype(np.int64))
+    # a single constant-TV bootstrap follows the phase half-torus
+    big = np.array([-100, -50, 50, 100], dtype=np.int64)
+    sm = toy_ref.keyswitch(toy_ref.encrypt_ints(big, seed=8))
+    out = toy_ref.pbs_const(sm, 1 << 61)
+    ph = toy_ref.phase(out).view(np.int64)
+    assert np.array_equal(ph > 0, big >= 0)
+
+
+def test_real_params_roundtrip(oracle_lib):
+    p = params_for_bits(16)
+    ref = oracle_lib.RefTFHE(p.as_dict(), 5)
+    assert ref.bsk.size == p.n * 3 * p.pbs_level * 3 * p.N
+    v = np.array([-32768, -1, 0, 12345, 32767], dtype=np.int64)
+    ct = ref.encrypt_ints(v, seed=1)
+    assert np.array_equal(ref.decrypt_ints(ct), v)
+    sm = ref.keyswitch(ct)
+    err = ref.phase(sm, small=True).view(np.int64) - (v << 48)
+    assert np.abs(err).max() < 2 ** 58

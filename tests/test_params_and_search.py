@@ -1,0 +1,84 @@
+"""CPU: parameter selection / noise model, and the sharded search merge over a
+2-rank gloo group (the N > 1 path of bench.py and search, without a GPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from fheicp.params import PBS_GADGETS, params_for_bits, noise_report
+from fheicp.search import sharded_topk
+
+
+@pytest.mark.parametrize("pmax,beta,lvl", PBS_GADGETS)
+def test_gadget_table_has_margin(pmax, beta, lvl):
+    p = params_for_bits(pmax)
+    assert (p.pbs_base_log, p.pbs_level) == (beta, lvl)
+    r = noise_report(p)
+    # >= 9.2 sigma at the 1/4-torus decision margin  <=>  p_fail <= 2^-64 per PBS
+    assert r["margin_sigmas"] > 9.2, r
+    assert r["log2_pfail_per_pbs"] < -64
+
+
+def test_params_for_bits_limits():
+    assert params_for_bits(11).pbs_level == 2
+    assert params_for_bits(21).pbs_level == 3
+    with pytest.raises(ValueError):
+        params_for_bits(28)
+
+
+def cpu_topk(acc, below, k, base_idx):
+    """Reference top-k for the test: Python stable sort, (acc desc, idx asc)."""
+    a = acc.tolist()
+    b = below.tolist() if below is not None else [0] * len(a)
+    keep = [(i, a[i]) for i in range(len(a)) if not b[i]]
+    keep.sort(key=lambda x: x[1], reverse=True)
+    keep = keep[:k]
+    oa = torch.full((k,), -(2 ** 63), dtype=torch.int64)
+    oi = torch.full((k,), -1, dtype=torch.int64)
+    for j, (i, v) in enumerate(keep):
+        oa[j] = v
+        oi[j] = i + base_idx
+    return oa, oi
+
+
+def _worker(rank, world, port, acc_all, below_all, k, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    n = len(acc_all) // world
+    acc = torch.tensor(acc_all[rank * n:(rank + 1) * n])
+    below = torch.tensor(below_all[rank * n:(rank + 1) * n])
+    oa, oi = sharded_topk(acc, below, k, rank * n, cpu_topk, world)
+    q.put((rank, oa.tolist(), oi.tolist()))
+    torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,k", [(2, 10), (2, 37), (4, 5)])
+def test_sharded_topk_equals_global(world, k):
+    rng = np.random.default_rng(world * 100 + k)
+    n = 64 * world
+    acc_all = rng.integers(-15, 15, n).tolist()          # many ties across shards
+    below_all = (rng.random(n) < 0.4).astype(np.int64).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, acc_all, below_all, k, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    ga, gi = cpu_topk(torch.tensor(acc_all), torch.tensor(below_all), k, 0)
+    for _, oa, oi in res:
+        assert oa == ga.tolist() and oi == gi.tolist()
