@@ -22,6 +22,7 @@
 #include "../../include/fhe_icp.h"
 #include "prng.h"
 #include "wave_fft.h"
+#include "br_m512.h"
 
 using namespace fhei;
 typedef uint64_t u64;
@@ -247,51 +248,85 @@ __global__ void __launch_bounds__(256) k_linear(const u64* __restrict__ ct, int 
   out[(size_t)b * W + t] = acc;
 }
 
-// Key switch, tiled: a workgroup owns TC ciphertexts x 256 output columns.
-// Digits of (a_i << shift) for the TC ciphertexts are staged in LDS per
-// chunk of IC inputs; every KSK word read feeds TC multiply-adds.
-constexpr int KS_TC = 32, KS_IC = 32;
+// Key switch (big -> small key), as a split-K integer GEMM:
+//   out[c][t] = body_c + (B/2) colsum[t] - sum_{i,l} d'[c][i][l] * KSK[i][l][t]
+// with offset-binary digits d' = d + B/2 in [0, B) (so each term is two
+// v_mad_u64_u32 on the 32-bit halves of the KSK word) and
+// colsum[t] = sum over all rows of KSK[.][t] (precomputed at keygen).
+// Workgroup = KS_TC ciphertexts x 256 output columns x one slice of the
+// input rows; slices are combined with u64 atomics, which are exact and
+// order-independent modulo 2^64 (bit-identical results every run).
+constexpr int KS_TC = 16, KS_IC = 32, KS_SPLIT = 8;
 __global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, int64_t count, int big, int n,
                                                    int KL, int kbeta, int shift, u64 add_body,
-                                                   const u64* __restrict__ ksk, u64* __restrict__ out) {
-  __shared__ int8_t dig[KS_TC][KS_IC][8];
+                                                   const u64* __restrict__ ksk, const u64* __restrict__ colsum,
+                                                   u64* __restrict__ out) {
+  __shared__ uint8_t dig[KS_IC][8][KS_TC];  // [input][level][ciphertext]
   const int col = blockIdx.x * 256 + threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.y * KS_TC;
   const int nct = (int)min((int64_t)KS_TC, count - c0);
-  u64 acc[KS_TC];
+  const int per = (big + KS_SPLIT - 1) / KS_SPLIT;
+  const int ibeg = blockIdx.z * per, iend_all = min(big, ibeg + per);
+  const u64 half = 1ull << (kbeta - 1);
+  u64 lo[KS_TC], hi[KS_TC];
 #pragma unroll
-  for (int q = 0; q < KS_TC; ++q) acc[q] = 0;
-  for (int i0 = 0; i0 < big; i0 += KS_IC) {
+  for (int q = 0; q < KS_TC; ++q) lo[q] = hi[q] = 0;
+  for (int i0 = ibeg; i0 < iend_all; i0 += KS_IC) {
     for (int e = threadIdx.x; e < KS_TC * KS_IC; e += 256) {
       const int q = e / KS_IC, ii = e % KS_IC;
-      if (q < nct && i0 + ii < big) {
+      if (q < nct && i0 + ii < iend_all) {
         const u64 a = in[(size_t)(c0 + q) * (big + 1) + i0 + ii] << shift;
-        const u64 packed = decompose_packed(a, kbeta, KL);
-        for (int l = 1; l <= KL; ++l) dig[q][ii][l - 1] = (int8_t)digit_of(packed, l, kbeta, KL);
+        const u64 packed = decompose_packed(a, kbeta, KL);  // offset-binary already
+        for (int l = 1; l <= KL; ++l) dig[ii][l - 1][q] = (uint8_t)((packed >> ((KL - l) * kbeta)) & ((1u << kbeta) - 1));
       } else {
-        for (int l = 0; l < KL; ++l) dig[q][ii][l] = 0;
+        for (int l = 0; l < KL; ++l) dig[ii][l][q] = (uint8_t)half;  // digit 0
       }
     }
     __syncthreads();
     if (col <= n) {
-      const int iend = min(KS_IC, big - i0);
-      for (int ii = 0; ii < iend; ++ii) {
+      const int cnt = min(KS_IC, iend_all - i0);
+      for (int ii = 0; ii < cnt; ++ii) {
         for (int l = 0; l < KL; ++l) {
           const u64 kv = ksk[((size_t)(i0 + ii) * KL + l) * (n + 1) + col];
+          const uint32_t kl = (uint32_t)kv, kh = (uint32_t)(kv >> 32);
+          const uint32_t* d4 = (const uint32_t*)&dig[ii][l][0];
 #pragma unroll
-          for (int q = 0; q < KS_TC; ++q) acc[q] -= (u64)(int64_t)dig[q][ii][l] * kv;
+          for (int w = 0; w < KS_TC / 4; ++w) {
+            const uint32_t pk = d4[w];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const uint32_t d = (pk >> (8 * b)) & 0xFF;
+              lo[4 * w + b] += (u64)d * kl;
+              hi[4 * w + b] += (u64)d * kh;
+            }
+          }
         }
       }
     }
     __syncthreads();
   }
   if (col <= n) {
-    for (int q = 0; q < nct; ++q) {
-      u64 v = acc[q];
-      if (col == n) v += (in[(size_t)(c0 + q) * (big + 1) + big] << shift) + add_body;
-      out[(size_t)(c0 + q) * (n + 1) + col] = v;
+#pragma unroll
+    for (int q = 0; q < KS_TC; ++q) {
+      if (q < nct) {
+        u64 v = (u64)0 - (lo[q] + (hi[q] << 32));
+        if (blockIdx.z == 0) {
+          v += half * colsum[col];
+          if (col == n) v += (in[(size_t)(c0 + q) * (big + 1) + big] << shift) + add_body;
+        }
+        atomicAdd((unsigned long long*)&out[(size_t)(c0 + q) * (n + 1) + col], (unsigned long long)v);
+      }
     }
   }
+}
+
+// colsum[t] = sum over all KSK rows of KSK[row][t] (mod 2^64)
+__global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, u64* __restrict__ colsum) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > n) return;
+  u64 s = 0;
+  for (int r = 0; r < rows; ++r) s += ksk[(size_t)r * (n + 1) + t];
+  colsum[t] = s;
 }
 
 // Blind rotation + sample extraction. One 64-lane wavefront (= workgroup)
@@ -430,6 +465,145 @@ __global__ void k_dequantize(const int64_t* __restrict__ acc, int64_t B, double 
   if (i < B) out[i] = out_scale * (double)acc[i];
 }
 
+// ---- v2 blind rotation, N = 1024: two waves per ciphertext (br_m512.h) ----
+// BSK conversion for v2: one 128-thread workgroup per polynomial, same FFT
+// as the blind rotation, stored at [u][tid] (LCs layout) and scaled by 1/M.
+__global__ void __launch_bounds__(128) k_bsk_to_fft_m512(const u64* __restrict__ bsk, int npoly,
+                                                         const c64* __restrict__ tw, const c64* __restrict__ twist,
+                                                         c64* __restrict__ out) {
+  using namespace m512;
+  __shared__ c64 lds[M + M / 8];
+  const int poly = blockIdx.x, tid = threadIdx.x;
+  if (poly >= npoly) return;
+  Tw T;
+  load_twiddles(T, tw, tid);
+  const u64* src = bsk + (size_t)poly * N;
+  c64 v[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) {
+    const int t = tcoef(tid, u);
+    v[u] = cmul({(double)(int64_t)src[t], (double)(int64_t)src[t + M]}, twist[t]);
+  }
+  forward(v, T, lds, tid);
+  const double inv = 1.0 / (double)M;
+  c64* dst = out + (size_t)poly * M;
+#pragma unroll
+  for (int u = 0; u < S; ++u) dst[fslot(tid, u)] = {v[u].x * inv, v[u].y * inv};
+}
+
+template <int K>
+__global__ void __launch_bounds__(128, 2) k_blind_rotate_m512(const u64* __restrict__ small, int n, int L, int beta,
+                                                              const c64* __restrict__ bsk, const c64* __restrict__ tw,
+                                                              const c64* __restrict__ twist, u64 tv, int mode,
+                                                              u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                              u64* __restrict__ refreshed, u64* __restrict__ sign) {
+  using namespace m512;
+  constexpr int LOG2N2 = 11;
+  __shared__ u64 acc[(K + 1) * N];
+  __shared__ c64 lds[M + M / 8];
+  const int tid = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const u64* sm = small + (size_t)c * (n + 1);
+  const int R = (K + 1) * L;
+
+  Tw T;
+  load_twiddles(T, tw, tid);
+  c64 twv[S];
+  int tc[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) {
+    tc[u] = tcoef(tid, u);
+    twv[u] = twist[tc[u]];
+  }
+
+  const uint32_t bt = modswitch_2n(sm[n], LOG2N2);
+  for (int t = tid; t < N; t += NT) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[j * N + t] = 0;
+    const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
+    acc[K * N + t] = idx < (uint32_t)N ? tv : (u64)0 - tv;
+  }
+  __syncthreads();
+
+  for (int i = 0; i < n; ++i) {
+    const uint32_t ai = modswitch_2n(sm[i], LOG2N2);
+    if (ai == 0) continue;
+    c64 outv[K + 1][S];
+#pragma unroll
+    for (int o = 0; o <= K; ++o)
+#pragma unroll
+      for (int u = 0; u < S; ++u) outv[o][u] = {0.0, 0.0};
+    const c64* G = bsk + (size_t)i * R * (K + 1) * M;
+#pragma unroll
+    for (int cc = 0; cc <= K; ++cc) {
+      const u64* f = acc + cc * N;
+      u64 p0[S], p1[S];
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const int t0 = tc[u], t1 = t0 + M;
+        const uint32_t i0 = (uint32_t)(t0 - (int)ai) & (2 * N - 1);
+        const uint32_t i1 = (uint32_t)(t1 - (int)ai) & (2 * N - 1);
+        const u64 r0 = i0 < (uint32_t)N ? f[i0] : (u64)0 - f[i0 - N];
+        const u64 r1 = i1 < (uint32_t)N ? f[i1] : (u64)0 - f[i1 - N];
+        p0[u] = decompose_packed(r0 - f[t0], beta, L);
+        p1[u] = decompose_packed(r1 - f[t1], beta, L);
+      }
+      for (int lvl = 1; lvl <= L; ++lvl) {
+        c64 v[S];
+#pragma unroll
+        for (int u = 0; u < S; ++u)
+          v[u] = cmul({(double)digit_of(p0[u], lvl, beta, L), (double)digit_of(p1[u], lvl, beta, L)}, twv[u]);
+        forward(v, T, lds, tid);
+        const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
+#pragma unroll
+        for (int o = 0; o <= K; ++o)
+#pragma unroll
+          for (int u = 0; u < S; ++u) cmac(outv[o][u], v[u], g[o * M + fslot(tid, u)]);
+      }
+    }
+    __syncthreads();  // every wave has read acc for this step
+#pragma unroll
+    for (int o = 0; o <= K; ++o) {
+      inverse(outv[o], T, lds, tid);
+#pragma unroll
+      for (int u = 0; u < S; ++u) {
+        const c64 z = cmulc(outv[o][u], twv[u]);
+        acc[o * N + tc[u]] += f64_to_torus(z.x);
+        acc[o * N + tc[u] + M] += f64_to_torus(z.y);
+      }
+    }
+    __syncthreads();
+  }
+
+  const int W = K * N + 1;
+  for (int j = 0; j < K; ++j) {
+    for (int t = tid; t < N; t += NT) {
+      const u64 a = (t == 0) ? acc[j * N] : (u64)0 - acc[j * N + N - t];
+      const size_t pos = (size_t)c * W + j * N + t;
+      if (mode == 0) {
+        out[pos] = a;
+      } else {
+        const u64 bit = (u64)0 - a;
+        ct_v[pos] -= bit;
+        refreshed[pos] += bit;
+        if (sign) sign[pos] = bit;
+      }
+    }
+  }
+  if (tid == 0) {
+    const size_t pos = (size_t)c * W + K * N;
+    const u64 b = acc[K * N];
+    if (mode == 0) {
+      out[pos] = b;
+    } else {
+      const u64 bit = tv - b;
+      ct_v[pos] -= bit;
+      refreshed[pos] += bit;
+      if (sign) sign[pos] = bit;
+    }
+  }
+}
+
 // acc_out[b] = v[b] + T
 __global__ void k_add_scalar(const int64_t* __restrict__ v, int64_t B, int64_t T, int64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -510,7 +684,7 @@ struct fhe_ctx {
   int device = -1;
   std::string err;
   bool keys = false;
-  u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr;
+  u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
   c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr;
   // workspace
   void* ws = nullptr;
@@ -633,7 +807,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
   if (!ctx) return;
   if (ctx->device >= 0) {
     hipSetDevice(ctx->device);
-    hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk);
+    hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk); hipFree(ctx->ksk_colsum);
     hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_ks);
@@ -671,17 +845,20 @@ static int alloc_keys(fhe_ctx* ctx) {
   HIPCHK(ctx, hipMalloc(&ctx->s_big, 8 * (size_t)p.k * p.N));
   HIPCHK(ctx, hipMalloc(&ctx->bsk, 8 * fhe_bsk_words(&p)));
   HIPCHK(ctx, hipMalloc(&ctx->ksk, 8 * fhe_ksk_words(&p)));
+  HIPCHK(ctx, hipMalloc(&ctx->ksk_colsum, 8 * (size_t)(p.n + 1)));
   HIPCHK(ctx, hipMalloc(&ctx->bsk_fft, sizeof(c64) * fhe_bsk_words(&p) / 2));
   return FHE_OK;
 }
 
 static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
   const fhe_params& p = ctx->p;
+  hipLaunchKernelGGL(k_ksk_colsum, dim3((p.n + 1 + 255) / 256), dim3(256), 0, st, ctx->ksk, p.k * p.N * p.ks_level,
+                     p.n, ctx->ksk_colsum);
   const int npoly = (int)(fhe_bsk_words(&p) / p.N);
   switch (p.N) {
     case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
     case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
-    case 1024: hipLaunchKernelGGL(k_bsk_to_fft<9>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
+    case 1024: hipLaunchKernelGGL(k_bsk_to_fft_m512, dim3(npoly), dim3(128), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
     case 2048: hipLaunchKernelGGL(k_bsk_to_fft<10>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
   }
   HIPCHK(ctx, hipGetLastError());
@@ -828,10 +1005,12 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   hipStream_t st = (hipStream_t)stream;
   const int64_t tiles = (count + KS_TC - 1) / KS_TC;
   if (tiles > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
+  HIPCHK(ctx, hipMemsetAsync(d_small, 0, 8 * (size_t)count * (p.n + 1), st));
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_ks, st, &e1);
-  hipLaunchKernelGGL(k_keyswitch, dim3((p.n + 1 + 255) / 256, (unsigned)tiles), dim3(256), 0, st, d_big, count,
-                     p.k * p.N, p.n, p.ks_level, p.ks_base_log, shift, add_body, ctx->ksk, d_small);
+  hipLaunchKernelGGL(k_keyswitch, dim3((p.n + 1 + 255) / 256, (unsigned)tiles, KS_SPLIT), dim3(256), 0, st, d_big,
+                     count, p.k * p.N, p.n, p.ks_level, p.ks_base_log, shift, add_body, ctx->ksk, ctx->ksk_colsum,
+                     d_small);
   prof_end(ctx, ctx->prof_ks, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
@@ -846,15 +1025,19 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint6
 #define BR(LOGM, K)                                                                                           \
   hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
                      ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
+#define BR2(K)                                                                                              \
+  hipLaunchKernelGGL((k_blind_rotate_m512<K>), g, dim3(128), 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log, \
+                     ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
   if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
   else if (p.N == 512 && p.k == 1) BR(8, 1);
   else if (p.N == 512 && p.k == 2) BR(8, 2);
-  else if (p.N == 1024 && p.k == 1) BR(9, 1);
-  else if (p.N == 1024 && p.k == 2) BR(9, 2);
+  else if (p.N == 1024 && p.k == 1) BR2(1);
+  else if (p.N == 1024 && p.k == 2) BR2(2);
   else if (p.N == 2048 && p.k == 1) BR(10, 1);
   else return fail(ctx, FHE_E_ARG, "unsupported (N, k)");
 #undef BR
+#undef BR2
   prof_end(ctx, ctx->prof_br, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;

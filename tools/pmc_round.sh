@@ -1,0 +1,14 @@
+#!/bin/bash
+# PMC passes over tools/prof_br.py (one rocprofv3 --pmc run per counter group).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
+timeout -k 10 300 python3 tools/prof_br.py > "$OUT/prof_br.txt" 2>&1 || exit 1
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o pmc --output-format csv -- python3 "$R/tools/prof_br.py" --rounds 1 > "$OUT/pmc$i.log" 2>&1 || { echo "pmc$i failed" >> "$OUT/pmc_status.txt"; exit 1; }
+  echo "pmc$i ok: $grp" >> "$OUT/pmc_status.txt"
+done
