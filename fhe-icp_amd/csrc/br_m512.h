@@ -11,7 +11,8 @@
 // layout maps each position to an index bit. Radix-2 stages run on slot
 // bits in registers; v_permlane32_swap exchanges slot bit 1 with lane bit 5
 // (a pure-VALU index-bit transposition), and an LDS relayout moves bits
-// between waves. Per FFT: 9 stages, 3 swaps, 2 LDS relayouts.
+// between waves. Per FFT: 9 stages, 3 swaps, 2 LDS relayouts (one across
+// the two waves with 2 barriers, one inside each wave with none).
 //   forward  LA[8,7] -swap-> LAs[6] -lds-> LB[5,4] -swap-> LBs[3] -lds-> LC[2,1] -swap-> LCs[0]
 //   inverse  the exact reverse, ending in LA (the coefficient layout).
 #pragma once
@@ -60,15 +61,46 @@ __device__ __forceinline__ void swap32(c64 (&v)[S]) {
   }
 }
 
-// LDS relayout between two layouts (both waves of the workgroup)
-__device__ __forceinline__ void relayout(c64 (&v)[S], const Lay& A, const Lay& B, c64* lds, int tid) {
+// LDS relayouts. Scratch hazards: a cross-wave relayout
+// writes or reads positions of BOTH waves' halves (split by index bit 8 in
+// LB/LBs/LC); a wave-local one only touches its own half. Barrier placement:
+//  - forward cross relayout (LAs -> LB): barrier BEFORE the writes (the
+//    other wave may still be reading its half from the previous FFT's
+//    wave-local relayout), writes, barrier, then reads of its own half;
+//  - inverse cross relayout (LB -> LAs): writes of its own half, barrier,
+//    reads across both halves, barrier AFTER (the next wave-local relayout
+//    writes into a half the other wave may still be reading).
+__device__ __forceinline__ void write_lay(const c64 (&v)[S], const Lay& A, c64* lds, int tid) {
 #pragma unroll
   for (int u = 0; u < S; ++u) lds[lds_pad(jof(A, tid, u))] = v[u];
-  __syncthreads();
+}
+__device__ __forceinline__ void read_lay(c64 (&v)[S], const Lay& B, const c64* lds, int tid) {
 #pragma unroll
   for (int u = 0; u < S; ++u) v[u] = lds[lds_pad(jof(B, tid, u))];
+}
+__device__ __forceinline__ void relayout_fwd(c64 (&v)[S], const Lay& A, const Lay& B, c64* lds, int tid) {
+  __syncthreads();
+  write_lay(v, A, lds, tid);
+  __syncthreads();
+  read_lay(v, B, lds, tid);
+}
+__device__ __forceinline__ void relayout_inv(c64 (&v)[S], const Lay& A, const Lay& B, c64* lds, int tid) {
+  write_lay(v, A, lds, tid);
+  __syncthreads();
+  read_lay(v, B, lds, tid);
   __syncthreads();
 }
+// Relayout inside one wave's half (same wave bit in both layouts): no
+// workgroup barrier. lgkmcnt(0) retires the wave's LDS writes before its
+// reads; the asm statements also pin the compiler's order.
+__device__ __forceinline__ void relayout_wave(c64 (&v)[S], const Lay& A, const Lay& B, c64* lds, int tid) {
+  write_lay(v, A, lds, tid);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  read_lay(v, B, lds, tid);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+static_assert(LB.p[8] == 8 && LBs.p[8] == 8 && LC.p[8] == 8, "wave halves must be split by index bit 8");
+static_assert(LBs.p[8] == LC.p[8], "LBs <-> LC must keep the wave bit");
 
 // Per-lane twiddles for the 9 stages, 2 butterflies each (loaded once).
 // Stage on slot bit sb of layout L at index bit k: butterflies (u, u|1<<sb)
@@ -125,30 +157,41 @@ __device__ __forceinline__ void forward(c64 (&v)[S], const Tw& T, c64* lds, int 
   dif<0>(v, T.w[7]);
   swap32(v);
   dif<1>(v, T.w[6]);
-  relayout(v, LAs, LB, lds, tid);
+  relayout_fwd(v, LAs, LB, lds, tid);
   dif<1>(v, T.w[5]);
   dif<0>(v, T.w[4]);
   swap32(v);
   dif<1>(v, T.w[3]);
-  relayout(v, LBs, LC, lds, tid);
+  relayout_wave(v, LBs, LC, lds, tid);
   dif<1>(v, T.w[2]);
   dif<0>(v, T.w[1]);
   swap32(v);
-  dif<1>(v, T.w[0]);
+  // stage 0: W = exp(0) = 1
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const c64 X = v[q], Y = v[q | 2];
+    v[q] = cadd(X, Y);
+    v[q | 2] = csub(X, Y);
+  }
 }
 
 // LCs -> LA, times M
 __device__ __forceinline__ void inverse(c64 (&v)[S], const Tw& T, c64* lds, int tid) {
-  dit<1>(v, T.w[0]);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // stage 0: W = 1
+    const c64 X = v[q], Y = v[q | 2];
+    v[q] = cadd(X, Y);
+    v[q | 2] = csub(X, Y);
+  }
   swap32(v);
   dit<0>(v, T.w[1]);
   dit<1>(v, T.w[2]);
-  relayout(v, LC, LBs, lds, tid);
+  relayout_wave(v, LC, LBs, lds, tid);
   dit<1>(v, T.w[3]);
   swap32(v);
   dit<0>(v, T.w[4]);
   dit<1>(v, T.w[5]);
-  relayout(v, LB, LAs, lds, tid);
+  relayout_inv(v, LB, LAs, lds, tid);
   dit<1>(v, T.w[6]);
   swap32(v);
   dit<0>(v, T.w[7]);

@@ -549,16 +549,22 @@ __global__ void __launch_bounds__(128, 2) k_blind_rotate_m512(const u64* __restr
         p1[u] = decompose_packed(r1 - f[t1], beta, L);
       }
       for (int lvl = 1; lvl <= L; ++lvl) {
+        // issue this row's BSK loads first so they fly during the FFT
+        const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
+        c64 kb[K + 1][S];
+#pragma unroll
+        for (int o = 0; o <= K; ++o)
+#pragma unroll
+          for (int u = 0; u < S; ++u) kb[o][u] = g[o * M + fslot(tid, u)];
         c64 v[S];
 #pragma unroll
         for (int u = 0; u < S; ++u)
           v[u] = cmul({(double)digit_of(p0[u], lvl, beta, L), (double)digit_of(p1[u], lvl, beta, L)}, twv[u]);
         forward(v, T, lds, tid);
-        const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
 #pragma unroll
         for (int o = 0; o <= K; ++o)
 #pragma unroll
-          for (int u = 0; u < S; ++u) cmac(outv[o][u], v[u], g[o * M + fslot(tid, u)]);
+          for (int u = 0; u < S; ++u) cmac(outv[o][u], v[u], kb[o][u]);
       }
     }
     __syncthreads();  // every wave has read acc for this step

@@ -142,15 +142,18 @@ struct WaveFFT {
 };
 
 // f64 -> u64 modulo 2^64 for an (approximately) integral value of any
-// magnitude below 2^1023: subtract the nearest multiple of 2^64 exactly,
-// then round the remainder (|r| <= 2^63) to an integer.
+// magnitude below 2^1023: subtract the nearest multiple of 2^64 exactly
+// (|r| <= 2^63), then split r = hi * 2^32 + lo with hi, lo exact 32-bit
+// integers (native v_cvt_i32_f64 / v_cvt_u32_f64 instead of the long
+// generic f64 -> i64 sequence).
 __device__ __forceinline__ uint64_t f64_to_torus(double v) {
   const double two64 = 18446744073709551616.0;
   const double m = rint(v * (1.0 / two64));
-  double r = __fma_rn(-m, two64, v);  // exact
-  r = rint(r);
-  if (r >= 9223372036854775808.0) r -= two64;
-  return (uint64_t)(int64_t)r;
+  const double r = rint(__fma_rn(-m, two64, v));      // exact, |r| <= 2^63
+  const double hi = floor(r * (1.0 / 4294967296.0));  // |hi| <= 2^31
+  const double lo = __fma_rn(-hi, 4294967296.0, r);   // exact, in [0, 2^32)
+  const uint32_t hu = (uint32_t)(int32_t)(hi >= 2147483648.0 ? hi - 4294967296.0 : hi);
+  return ((uint64_t)hu << 32) + (uint64_t)(uint32_t)lo;
 }
 
 }  // namespace fhei

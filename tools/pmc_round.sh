@@ -7,7 +7,7 @@ timeout -k 10 300 python3 tools/prof_br.py > "$OUT/prof_br.txt" 2>&1 || exit 1
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR" \
-           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+           "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64" "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o pmc --output-format csv -- python3 "$R/tools/prof_br.py" --rounds 1 > "$OUT/pmc$i.log" 2>&1 || { echo "pmc$i failed" >> "$OUT/pmc_status.txt"; exit 1; }
   echo "pmc$i ok: $grp" >> "$OUT/pmc_status.txt"
