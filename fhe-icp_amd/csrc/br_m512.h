@@ -204,4 +204,18 @@ __device__ __forceinline__ int tcoef(int tid, int u) { return jof(LA, tid, u); }
 __device__ __forceinline__ int fslot(int tid, int u) { return u * NT + tid; }
 
 }  // namespace m512
+
+// Adapter used by the templated blind-rotation kernel (fheicp.hip).
+struct V2 {
+  static constexpr int M = m512::M, N = m512::N, S = m512::S, NT = m512::NT;
+  static constexpr bool MULTI = false;
+  static constexpr int SCRATCH = m512::M + m512::M / 8;
+  using Tw = m512::Tw;
+  __device__ static void load_twiddles(Tw& T, const c64* tw, int tid) { m512::load_twiddles(T, tw, tid); }
+  __device__ static void forward(c64 (&v)[S], const Tw& T, c64* lds, int tid) { m512::forward(v, T, lds, tid); }
+  __device__ static void inverse(c64 (&v)[S], const Tw& T, c64* lds, int tid) { m512::inverse(v, T, lds, tid); }
+  __device__ static int tcoef(int tid, int u) { return m512::tcoef(tid, u); }
+  __device__ static int fslot(int tid, int u) { return m512::fslot(tid, u); }
+};
+
 }  // namespace fhei

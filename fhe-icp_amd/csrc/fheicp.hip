@@ -23,6 +23,7 @@
 #include "prng.h"
 #include "wave_fft.h"
 #include "br_m512.h"
+#include "br_m512q.h"
 
 using namespace fhei;
 typedef uint64_t u64;
@@ -465,54 +466,60 @@ __global__ void k_dequantize(const int64_t* __restrict__ acc, int64_t B, double 
   if (i < B) out[i] = out_scale * (double)acc[i];
 }
 
-// ---- v2 blind rotation, N = 1024: two waves per ciphertext (br_m512.h) ----
+// ---- blind rotation for N = 1024, several waves per ciphertext -------------
+// V = V2 (br_m512.h: 2 waves, 4 complex/lane) or V3 (br_m512q.h: 4 waves,
+// 2 complex/lane); both share this kernel body.
 // BSK conversion for v2: one 128-thread workgroup per polynomial, same FFT
 // as the blind rotation, stored at [u][tid] (LCs layout) and scaled by 1/M.
-__global__ void __launch_bounds__(128) k_bsk_to_fft_m512(const u64* __restrict__ bsk, int npoly,
+template <class V>
+__global__ void __launch_bounds__(V::NT) k_bsk_to_fft_mw(const u64* __restrict__ bsk, int npoly,
                                                          const c64* __restrict__ tw, const c64* __restrict__ twist,
                                                          c64* __restrict__ out) {
-  using namespace m512;
-  __shared__ c64 lds[M + M / 8];
+  constexpr int M = V::M, N = V::N, S = V::S;
+  using Tw = typename V::Tw;
+  __shared__ c64 lds[V::SCRATCH];
   const int poly = blockIdx.x, tid = threadIdx.x;
   if (poly >= npoly) return;
   Tw T;
-  load_twiddles(T, tw, tid);
+  V::load_twiddles(T, tw, tid);
   const u64* src = bsk + (size_t)poly * N;
-  c64 v[S];
+  c64 v[1][S];
 #pragma unroll
   for (int u = 0; u < S; ++u) {
-    const int t = tcoef(tid, u);
-    v[u] = cmul({(double)(int64_t)src[t], (double)(int64_t)src[t + M]}, twist[t]);
+    const int t = V::tcoef(tid, u);
+    v[0][u] = cmul({(double)(int64_t)src[t], (double)(int64_t)src[t + M]}, twist[t]);
   }
-  forward(v, T, lds, tid);
+  if constexpr (V::MULTI) V::template forward<1>(v, T, lds, tid);
+  else V::forward(v[0], T, lds, tid);
   const double inv = 1.0 / (double)M;
   c64* dst = out + (size_t)poly * M;
 #pragma unroll
-  for (int u = 0; u < S; ++u) dst[fslot(tid, u)] = {v[u].x * inv, v[u].y * inv};
+  for (int u = 0; u < S; ++u) dst[V::fslot(tid, u)] = {v[0][u].x * inv, v[0][u].y * inv};
 }
 
-template <int K>
-__global__ void __launch_bounds__(128, 2) k_blind_rotate_m512(const u64* __restrict__ small, int n, int L, int beta,
+template <class V, int K, int MINW>
+__global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __restrict__ small, int n, int L, int beta,
                                                               const c64* __restrict__ bsk, const c64* __restrict__ tw,
                                                               const c64* __restrict__ twist, u64 tv, int mode,
                                                               u64* __restrict__ out, u64* __restrict__ ct_v,
                                                               u64* __restrict__ refreshed, u64* __restrict__ sign) {
-  using namespace m512;
+  constexpr int M = V::M, N = V::N, S = V::S, NT = V::NT;
+  using Tw = typename V::Tw;
   constexpr int LOG2N2 = 11;
   __shared__ u64 acc[(K + 1) * N];
-  __shared__ c64 lds[M + M / 8];
+  __shared__ c64 lds[V::SCRATCH];
   const int tid = threadIdx.x;
   const int64_t c = blockIdx.x;
   const u64* sm = small + (size_t)c * (n + 1);
   const int R = (K + 1) * L;
 
   Tw T;
-  load_twiddles(T, tw, tid);
+  V::load_twiddles(T, tw, tid);
   c64 twv[S];
   int tc[S];
 #pragma unroll
   for (int u = 0; u < S; ++u) {
-    tc[u] = tcoef(tid, u);
+    tc[u] = V::tcoef(tid, u);
     twv[u] = twist[tc[u]];
   }
 
@@ -548,29 +555,77 @@ __global__ void __launch_bounds__(128, 2) k_blind_rotate_m512(const u64* __restr
         p0[u] = decompose_packed(r0 - f[t0], beta, L);
         p1[u] = decompose_packed(r1 - f[t1], beta, L);
       }
-      for (int lvl = 1; lvl <= L; ++lvl) {
-        // issue this row's BSK loads first so they fly during the FFT
-        const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
-        c64 kb[K + 1][S];
+      if constexpr (V::MULTI) {
+        // levels in pairs: both forward FFTs share every relayout
+        for (int lvl = 1; lvl <= L; lvl += 2) {
+          if (lvl + 1 <= L) {
+            c64 v[2][S];
 #pragma unroll
-        for (int o = 0; o <= K; ++o)
+            for (int f = 0; f < 2; ++f)
 #pragma unroll
-          for (int u = 0; u < S; ++u) kb[o][u] = g[o * M + fslot(tid, u)];
-        c64 v[S];
+              for (int u = 0; u < S; ++u)
+                v[f][u] = cmul({(double)digit_of(p0[u], lvl + f, beta, L), (double)digit_of(p1[u], lvl + f, beta, L)},
+                               twv[u]);
+            V::template forward<2>(v, T, lds, tid);
 #pragma unroll
-        for (int u = 0; u < S; ++u)
-          v[u] = cmul({(double)digit_of(p0[u], lvl, beta, L), (double)digit_of(p1[u], lvl, beta, L)}, twv[u]);
-        forward(v, T, lds, tid);
+            for (int f = 0; f < 2; ++f) {
+              const c64* g = G + (size_t)((cc * L + lvl + f - 1) * (K + 1)) * M;
 #pragma unroll
-        for (int o = 0; o <= K; ++o)
+              for (int o = 0; o <= K; ++o)
 #pragma unroll
-          for (int u = 0; u < S; ++u) cmac(outv[o][u], v[u], kb[o][u]);
+                for (int u = 0; u < S; ++u) cmac(outv[o][u], v[f][u], g[o * M + V::fslot(tid, u)]);
+            }
+          } else {
+            c64 v[1][S];
+#pragma unroll
+            for (int u = 0; u < S; ++u)
+              v[0][u] = cmul({(double)digit_of(p0[u], lvl, beta, L), (double)digit_of(p1[u], lvl, beta, L)}, twv[u]);
+            V::template forward<1>(v, T, lds, tid);
+            const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
+#pragma unroll
+            for (int o = 0; o <= K; ++o)
+#pragma unroll
+              for (int u = 0; u < S; ++u) cmac(outv[o][u], v[0][u], g[o * M + V::fslot(tid, u)]);
+          }
+        }
+      } else {
+        for (int lvl = 1; lvl <= L; ++lvl) {
+          // issue this row's BSK loads first so they fly during the FFT
+          const c64* g = G + (size_t)((cc * L + lvl - 1) * (K + 1)) * M;
+          c64 kb[K + 1][S];
+#pragma unroll
+          for (int o = 0; o <= K; ++o)
+#pragma unroll
+            for (int u = 0; u < S; ++u) kb[o][u] = g[o * M + V::fslot(tid, u)];
+          c64 v[S];
+#pragma unroll
+          for (int u = 0; u < S; ++u)
+            v[u] = cmul({(double)digit_of(p0[u], lvl, beta, L), (double)digit_of(p1[u], lvl, beta, L)}, twv[u]);
+          V::forward(v, T, lds, tid);
+#pragma unroll
+          for (int o = 0; o <= K; ++o)
+#pragma unroll
+            for (int u = 0; u < S; ++u) cmac(outv[o][u], v[u], kb[o][u]);
+        }
       }
     }
     __syncthreads();  // every wave has read acc for this step
+    if constexpr (V::MULTI) {
+      // outputs in pairs (the scratch holds two polynomials)
+#pragma unroll
+      for (int o = 0; o <= K; o += 2) {
+        if (o + 1 <= K) {
+          V::template inverse<2>(*reinterpret_cast<c64(*)[2][S]>(&outv[o]), T, lds, tid);
+        } else {
+          V::template inverse<1>(*reinterpret_cast<c64(*)[1][S]>(&outv[o]), T, lds, tid);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o <= K; ++o) V::inverse(outv[o], T, lds, tid);
+    }
 #pragma unroll
     for (int o = 0; o <= K; ++o) {
-      inverse(outv[o], T, lds, tid);
 #pragma unroll
       for (int u = 0; u < S; ++u) {
         const c64 z = cmulc(outv[o][u], twv[u]);
@@ -697,6 +752,7 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
   bool prof = false;
   ProfAcc prof_br, prof_ks;
+  int br_variant = 2;  // N=1024 blind rotation: 2 = two waves/ct (default), 3 = four waves/ct
 };
 
 static std::mutex g_err_mu;
@@ -769,6 +825,7 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   fhe_ctx* ctx = new fhe_ctx();
   ctx->p = *params;
   ctx->device = device;
+  if (const char* e = getenv("FHEICP_BR_VARIANT")) ctx->br_variant = atoi(e) == 3 ? 3 : 2;
   if (device >= 0) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
@@ -864,7 +921,12 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
   switch (p.N) {
     case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
     case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
-    case 1024: hipLaunchKernelGGL(k_bsk_to_fft_m512, dim3(npoly), dim3(128), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
+    case 1024:
+      if (ctx->br_variant == 3)
+        hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
+      else
+        hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
+      break;
     case 2048: hipLaunchKernelGGL(k_bsk_to_fft<10>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
   }
   HIPCHK(ctx, hipGetLastError());
@@ -1031,9 +1093,10 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint6
 #define BR(LOGM, K)                                                                                           \
   hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
                      ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
-#define BR2(K)                                                                                              \
-  hipLaunchKernelGGL((k_blind_rotate_m512<K>), g, dim3(128), 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log, \
-                     ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
+#define BRV(V, K, W)                                                                                          \
+  hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,          \
+                     p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
+#define BR2(K) do { if (ctx->br_variant == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
   if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
   else if (p.N == 512 && p.k == 1) BR(8, 1);
@@ -1044,6 +1107,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint6
   else return fail(ctx, FHE_E_ARG, "unsupported (N, k)");
 #undef BR
 #undef BR2
+#undef BRV
   prof_end(ctx, ctx->prof_br, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;

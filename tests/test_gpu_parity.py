@@ -172,3 +172,15 @@ def test_topk_matches_stable_sort(need_gpu):
         assert [int(i) - 100 for i in got_i[:len(exp)]] == [i for i, _ in exp]
         assert [int(a) for a in got_a[:len(exp)]] == [a for _, a in exp]
         assert np.all(got_i[len(exp):] == -1)
+
+
+def test_bit_extract_real_params_v3_kernel(need_gpu, oracle_lib, monkeypatch):
+    """The 4-wave blind rotation (FHEICP_BR_VARIANT=3) gives the same results."""
+    monkeypatch.setenv("FHEICP_BR_VARIANT", "3")
+    eng = Engine(REAL16, 0)
+    eng.keygen(777)
+    P = eng.msg_bits
+    v = np.random.default_rng(19).integers(-(2 ** (P - 1)), 2 ** (P - 1), 128)
+    ref_ct, sign = eng.bit_extract(eng.encrypt(v, seed=22))
+    assert np.array_equal(eng.decrypt(ref_ct).cpu().numpy(), v)
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
