@@ -1250,6 +1250,52 @@ int fhe_topk(fhe_ctx* ctx, const int64_t* d_acc, const int64_t* d_below, int64_t
   return FHE_OK;
 }
 
+int fhe_dev_alloc(fhe_ctx* ctx, size_t bytes, void** d_out) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (!d_out) return fail(ctx, FHE_E_ARG, "null output pointer");
+  *d_out = nullptr;
+  if (bytes == 0) return FHE_OK;
+  if (hipMalloc(d_out, bytes) != hipSuccess) {
+    *d_out = nullptr;
+    return fail(ctx, FHE_E_NOMEM, "hipMalloc failed");
+  }
+  return FHE_OK;
+}
+
+int fhe_dev_free(fhe_ctx* ctx, void* d_ptr) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (d_ptr) HIPCHK(ctx, hipFree(d_ptr));
+  return FHE_OK;
+}
+
+int fhe_memcpy_h2d(fhe_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (bytes == 0) return FHE_OK;
+  if (!d_dst || !h_src) return fail(ctx, FHE_E_ARG, "null copy pointer");
+  HIPCHK(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return FHE_OK;
+}
+
+int fhe_memcpy_d2h(fhe_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (bytes == 0) return FHE_OK;
+  if (!h_dst || !d_src) return fail(ctx, FHE_E_ARG, "null copy pointer");
+  HIPCHK(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+  return FHE_OK;
+}
+
+int fhe_stream_sync(fhe_ctx* ctx, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+  return FHE_OK;
+}
+
 int fhe_profile_enable(fhe_ctx* ctx, int enable) {
   if (!ctx) return fail(nullptr, FHE_E_ARG, "null ctx");
   ctx->prof = enable != 0;

@@ -55,6 +55,11 @@ SIGNATURES = [
     ("fhe_quantize_pairs", C.c_int, [_CTXP, _vp, _i32, _vp, _i32, _i64, _i32, C.c_double, _i64, _i64, _i64, _vp, _vp]),
     ("fhe_dequantize", C.c_int, [_CTXP, _vp, _i64, C.c_double, _vp, _vp]),
     ("fhe_topk", C.c_int, [_CTXP, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    ("fhe_dev_alloc", C.c_int, [_CTXP, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("fhe_dev_free", C.c_int, [_CTXP, _vp]),
+    ("fhe_memcpy_h2d", C.c_int, [_CTXP, _vp, _vp, C.c_size_t, _vp]),
+    ("fhe_memcpy_d2h", C.c_int, [_CTXP, _vp, _vp, C.c_size_t, _vp]),
+    ("fhe_stream_sync", C.c_int, [_CTXP, _vp]),
     ("fhe_profile_enable", C.c_int, [_CTXP, C.c_int]),
     ("fhe_profile_read", C.c_int, [_CTXP, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64), C.POINTER(_i64)]),
 ]

@@ -1,0 +1,54 @@
+"""Versioned persistence of a compiled model: quantisation parameters + keys.
+
+The reference cannot persist a compiled model (fhe_similarity.py:176-182,
+:215-220 forces a retrain after load) and retrains + recompiles in every
+process (batch_operations.py:78-108), so its results change run to run.
+This file format makes a model reproducible across processes and GPUs
+(SURVEY.md §8f-2):
+
+    npz (no pickles; load with allow_pickle=False)
+      meta     uint8[]  UTF-8 JSON {"format": "fheicp-model", "version": 1,
+                        "quant": QuantParams.to_dict(), "scheme": SchemeParams}
+      s_small, s_big, bsk, ksk   uint64[]  (optional; fhe_export_keys layout)
+
+The key arrays hold the SECRET keys: protect the file like the reference's
+key directory (key_management.py stores Fernet-encrypted blobs; the
+``cryptography`` package is not available in this image, so wrapping the
+file is left to the caller).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+from .model import QuantParams
+from .params import SchemeParams
+
+FORMAT = "fheicp-model"
+VERSION = 1
+KEY_NAMES = ("s_small", "s_big", "bsk", "ksk")
+
+
+def save_model(path: str, qparams: QuantParams, scheme: SchemeParams, keys: dict | None = None) -> None:
+    meta = {"format": FORMAT, "version": VERSION, "quant": qparams.to_dict(), "scheme": scheme.as_dict()}
+    arrays = {"meta": np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)}
+    if keys is not None:
+        for k in KEY_NAMES:
+            arrays[k] = np.ascontiguousarray(keys[k], dtype=np.uint64)
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, **arrays)
+    os.replace(tmp, path)
+
+
+def load_model(path: str):
+    """-> (QuantParams, SchemeParams, keys dict or None)."""
+    with np.load(path, allow_pickle=False) as z:
+        meta = json.loads(bytes(z["meta"]).decode())
+        if meta.get("format") != FORMAT:
+            raise ValueError(f"{path}: not an {FORMAT} file")
+        if int(meta.get("version", 0)) > VERSION:
+            raise ValueError(f"{path}: format version {meta['version']} is newer than supported {VERSION}")
+        keys = {k: z[k].copy() for k in KEY_NAMES} if all(k in z.files for k in KEY_NAMES) else None
+    return QuantParams.from_dict(meta["quant"]), SchemeParams(**meta["scheme"]), keys

@@ -129,10 +129,12 @@ int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_
  * One call per batch of B (query, document) pairs — the batched replacement
  * of the per-document loop at batch_operations.py:268-279 and of
  * compare_encrypted (batch_operations.py:206-238):
- *   encrypt q_x (B x D) -> linear with d_w and cst - T -> bit extraction ->
- *   decrypt. d_acc[b] = the decrypted accumulator (exact int64, = Concrete's
- *   q_x @ q_w - zp*sum(q_w) + q_b), d_below[b] = 1 iff acc < T (decrypted
- *   encrypted threshold bit; acc >= T <=> score >= min_similarity).
+ *   encrypt q_x (B x D) -> linear with d_w and cst - T -> decrypt the
+ *   leveled accumulator -> bit extraction (msg_bits KS + PBS) -> decrypt the
+ *   sign bit. d_acc[b] = the decrypted accumulator (exact int64, = Concrete's
+ *   q_x @ q_w - zp*sum(q_w) + q_b; read from the leveled ciphertext like the
+ *   reference's leveled circuit), d_below[b] = 1 iff acc < T (the decrypted
+ *   bootstrapped threshold bit; acc >= T <=> score >= min_similarity).
  * Uses context-owned workspace (grown on demand; not graph-capturable). */
 int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                       int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream);
@@ -155,6 +157,16 @@ int fhe_dequantize(fhe_ctx* ctx, const int64_t* d_acc, int64_t B, double out_sca
  * base_idx + position. Missing slots get acc = INT64_MIN, idx = -1. */
 int fhe_topk(fhe_ctx* ctx, const int64_t* d_acc, const int64_t* d_below, int64_t B, int64_t base_idx, int32_t k,
              int64_t* d_out_acc, int64_t* d_out_idx, void* stream);
+
+/* ---- device memory -------------------------------------------------------
+ * For callers without a device allocator of their own (a ctypes binding from
+ * numpy); torch callers pass tensor pointers instead.
+ * fhe_memcpy_d2h returns after the copy completed (it synchronises `stream`). */
+int fhe_dev_alloc(fhe_ctx* ctx, size_t bytes, void** d_out);
+int fhe_dev_free(fhe_ctx* ctx, void* d_ptr);
+int fhe_memcpy_h2d(fhe_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream);
+int fhe_memcpy_d2h(fhe_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream);
+int fhe_stream_sync(fhe_ctx* ctx, void* stream);
 
 /* ---- measurement ------------------------------------------------------------
  * When enabled, every blind-rotation (external-product) and key-switch

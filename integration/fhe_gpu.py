@@ -1,0 +1,104 @@
+"""Reference-side ctypes binding of libfheicp.so (no torch, numpy only).
+
+This is the file a maintainer of the reference would add next to
+fhe_similarity.py to call the MI355X engine through its C ABI
+(include/fhe_icp.h) directly; INTEGRATION.md shows where it plugs in. It is
+kept here, runnable, so tests/test_gpu_dropin.py can prove that the binding
+works as written.
+
+    eng = GpuCompare(params_dict, key_seed=1234, lib_path=".../libfheicp.so")
+    acc, below = eng.compare(q_x, q_w, cst, T)   # int64 numpy arrays
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
+          "lwe_noise_bits", "glwe_noise_bits", "msg_bits")
+
+
+class fhe_params(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in FIELDS]
+
+
+_vp, _i32, _i64, _u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+_PROTOS = {
+    "fhe_ctx_create": (C.c_int, [C.POINTER(fhe_params), C.c_int, C.POINTER(_vp)]),
+    "fhe_ctx_destroy": (None, [_vp]),
+    "fhe_last_error": (C.c_char_p, [_vp]),
+    "fhe_keygen": (C.c_int, [_vp, _u64, _vp]),
+    "fhe_dev_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
+    "fhe_dev_free": (C.c_int, [_vp, _vp]),
+    "fhe_memcpy_h2d": (C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp]),
+    "fhe_memcpy_d2h": (C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp]),
+    "fhe_compare_batch": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
+    "fhe_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+}
+
+
+class GpuCompare:
+    """One device context + keys; batched encrypted compares from numpy."""
+
+    def __init__(self, params: dict, key_seed: int, device: int = 0, lib_path: str | None = None,
+                 enc_seed: int | None = None):
+        path = lib_path or os.environ.get("FHEICP_LIB", "libfheicp.so")
+        self.L = L = C.CDLL(path)
+        for name, (res, args) in _PROTOS.items():
+            getattr(L, name).restype = res
+            getattr(L, name).argtypes = args
+        self.P = fhe_params(**{f: int(params[f]) for f in FIELDS})
+        self.ctx = _vp()
+        self._ok(L.fhe_ctx_create(C.byref(self.P), device, C.byref(self.ctx)))
+        self._ok(L.fhe_keygen(self.ctx, key_seed, None))
+        self.enc_seed = enc_seed if enc_seed is not None else key_seed ^ 0x5DEECE66D
+        self.next_id = 0
+
+    def _ok(self, rc: int) -> None:
+        if rc != 0:
+            msg = self.L.fhe_last_error(self.ctx if self.ctx else None)
+            raise RuntimeError(f"libfheicp error {rc}: {msg.decode() if msg else ''}")
+
+    def _to_dev(self, a: np.ndarray) -> _vp:
+        a = np.ascontiguousarray(a)
+        d = _vp()
+        self._ok(self.L.fhe_dev_alloc(self.ctx, a.nbytes, C.byref(d)))
+        self._ok(self.L.fhe_memcpy_h2d(self.ctx, d, a.ctypes.data, a.nbytes, None))
+        return d
+
+    def _alloc(self, nbytes: int) -> _vp:
+        d = _vp()
+        self._ok(self.L.fhe_dev_alloc(self.ctx, nbytes, C.byref(d)))
+        return d
+
+    def _to_host(self, d: _vp, count: int) -> np.ndarray:
+        out = np.empty(count, np.int64)
+        self._ok(self.L.fhe_memcpy_d2h(self.ctx, out.ctypes.data, d, out.nbytes, None))
+        return out
+
+    def compare(self, q_x: np.ndarray, q_w: np.ndarray, cst: int, T: int):
+        """Encrypted compare of B quantized feature rows: (acc int64[B], below int64[B])."""
+        q_x = np.asarray(q_x, np.int64)
+        B, D = q_x.shape
+        bufs = [self._to_dev(q_x), self._to_dev(np.asarray(q_w, np.int64)), self._alloc(8 * B), self._alloc(8 * B)]
+        try:
+            self._ok(self.L.fhe_compare_batch(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(T), self.enc_seed,
+                                              self.next_id, bufs[2], bufs[3], None))
+            self.next_id += B * D
+            return self._to_host(bufs[2], B), self._to_host(bufs[3], B)
+        finally:
+            for d in bufs:
+                self.L.fhe_dev_free(self.ctx, d)
+
+    def close(self) -> None:
+        if self.ctx:
+            self.L.fhe_ctx_destroy(self.ctx)
+            self.ctx = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
