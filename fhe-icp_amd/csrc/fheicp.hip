@@ -330,16 +330,44 @@ __global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, u64* 
   colsum[t] = s;
 }
 
+// Test vector of a bootstrap: TV_j = base + (j >> shift) * step for
+// j in [0, N) (a staircase; step = 0 gives the constant TV of a sign
+// bootstrap), extended negacyclically: coefficient t of X^{-b} TV is
+// TV_{(t+b) mod 2N} with a minus sign when (t + b) mod 2N >= N.
+struct BrTv {
+  u64 base, step;
+  int shift;
+};
+__device__ __forceinline__ u64 tv_rot(const BrTv& tv, uint32_t idx, int N) {
+  const uint32_t j = idx & (uint32_t)(N - 1);
+  const u64 v = tv.base + (u64)(j >> tv.shift) * tv.step;
+  return idx < (uint32_t)N ? v : (u64)0 - v;
+}
+// Output of one extracted LWE word x (word `pos` of ciphertext c):
+//   mode 0: out = x
+//   mode 1: sign-bit round: bit = trivial(tv.base) - x; ct_v -= bit;
+//           refreshed += bit (if given); sign = bit (if given)
+//   mode 2: digit round: ct_v -= x; refreshed += x (if given)
+__device__ __forceinline__ void br_emit(int mode, u64 x, bool body, const BrTv& tv, size_t pos, u64* out, u64* ct_v,
+                                        u64* refreshed, u64* sign) {
+  if (mode == 0) {
+    out[pos] = x;
+    return;
+  }
+  const u64 d = mode == 1 ? (body ? tv.base : (u64)0) - x : x;
+  ct_v[pos] -= d;
+  if (refreshed) refreshed[pos] += d;
+  if (sign) sign[pos] = d;
+}
+
 // Blind rotation + sample extraction. One 64-lane wavefront (= workgroup)
 // per ciphertext; the GLWE accumulator ((K+1) x N u64) lives in LDS, the
 // external-product partial sums in registers.
-//   mode 0: out[c] = extracted LWE (phase ~ +-tv)
-//   mode 1: bit extraction epilogue: bit = trivial(tv) - extracted;
-//           ct_v[c] -= bit; refreshed[c] += bit; sign[c] = bit if sign != 0.
+// Test vector and epilogue modes: BrTv / br_emit above.
 template <int LOGM, int K>
 __global__ void __launch_bounds__(64) k_blind_rotate(const u64* __restrict__ small, int n, int L, int beta,
                                                      const c64* __restrict__ bsk, const c64* __restrict__ tw,
-                                                     const c64* __restrict__ twist, u64 tv, int mode,
+                                                     const c64* __restrict__ twist, BrTv tv, int mode,
                                                      u64* __restrict__ out, u64* __restrict__ ct_v,
                                                      u64* __restrict__ refreshed, u64* __restrict__ sign) {
   using F = WaveFFT<LOGM>;
@@ -358,7 +386,7 @@ __global__ void __launch_bounds__(64) k_blind_rotate(const u64* __restrict__ sma
 #pragma unroll
     for (int j = 0; j < K; ++j) acc[j * N + t] = 0;
     const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
-    acc[K * N + t] = idx < (uint32_t)N ? tv : (u64)0 - tv;
+    acc[K * N + t] = tv_rot(tv, idx, N);
   }
   __syncthreads();
 
@@ -419,29 +447,10 @@ __global__ void __launch_bounds__(64) k_blind_rotate(const u64* __restrict__ sma
   for (int j = 0; j < K; ++j) {
     for (int t = l; t < N; t += 64) {
       const u64 a = (t == 0) ? acc[j * N] : (u64)0 - acc[j * N + N - t];
-      const size_t pos = (size_t)c * W + j * N + t;
-      if (mode == 0) {
-        out[pos] = a;
-      } else {
-        const u64 bit = (u64)0 - a;
-        ct_v[pos] -= bit;
-        refreshed[pos] += bit;
-        if (sign) sign[pos] = bit;
-      }
+      br_emit(mode, a, false, tv, (size_t)c * W + j * N + t, out, ct_v, refreshed, sign);
     }
   }
-  if (l == 0) {
-    const size_t pos = (size_t)c * W + K * N;
-    const u64 b = acc[K * N];
-    if (mode == 0) {
-      out[pos] = b;
-    } else {
-      const u64 bit = tv - b;
-      ct_v[pos] -= bit;
-      refreshed[pos] += bit;
-      if (sign) sign[pos] = bit;
-    }
-  }
+  if (l == 0) br_emit(mode, acc[K * N], true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
 }
 
 // Client-side input path of batch_operations.py:226/:273 + Concrete-ML's
@@ -500,7 +509,7 @@ __global__ void __launch_bounds__(V::NT) k_bsk_to_fft_mw(const u64* __restrict__
 template <class V, int K, int MINW>
 __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __restrict__ small, int n, int L, int beta,
                                                               const c64* __restrict__ bsk, const c64* __restrict__ tw,
-                                                              const c64* __restrict__ twist, u64 tv, int mode,
+                                                              const c64* __restrict__ twist, BrTv tv, int mode,
                                                               u64* __restrict__ out, u64* __restrict__ ct_v,
                                                               u64* __restrict__ refreshed, u64* __restrict__ sign) {
   constexpr int M = V::M, N = V::N, S = V::S, NT = V::NT;
@@ -528,7 +537,7 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
 #pragma unroll
     for (int j = 0; j < K; ++j) acc[j * N + t] = 0;
     const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
-    acc[K * N + t] = idx < (uint32_t)N ? tv : (u64)0 - tv;
+    acc[K * N + t] = tv_rot(tv, idx, N);
   }
   __syncthreads();
 
@@ -640,29 +649,10 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
   for (int j = 0; j < K; ++j) {
     for (int t = tid; t < N; t += NT) {
       const u64 a = (t == 0) ? acc[j * N] : (u64)0 - acc[j * N + N - t];
-      const size_t pos = (size_t)c * W + j * N + t;
-      if (mode == 0) {
-        out[pos] = a;
-      } else {
-        const u64 bit = (u64)0 - a;
-        ct_v[pos] -= bit;
-        refreshed[pos] += bit;
-        if (sign) sign[pos] = bit;
-      }
+      br_emit(mode, a, false, tv, (size_t)c * W + j * N + t, out, ct_v, refreshed, sign);
     }
   }
-  if (tid == 0) {
-    const size_t pos = (size_t)c * W + K * N;
-    const u64 b = acc[K * N];
-    if (mode == 0) {
-      out[pos] = b;
-    } else {
-      const u64 bit = tv - b;
-      ct_v[pos] -= bit;
-      refreshed[pos] += bit;
-      if (sign) sign[pos] = bit;
-    }
-  }
+  if (tid == 0) br_emit(mode, acc[K * N], true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
 }
 
 // acc_out[b] = v[b] + T
@@ -1084,7 +1074,7 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   return FHE_OK;
 }
 
-static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t tv, int mode, uint64_t* out,
+static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv tv, int mode, uint64_t* out,
                      uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, hipStream_t st) {
   const fhe_params& p = ctx->p;
   hipEvent_t e1;
@@ -1092,10 +1082,10 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint6
   const dim3 g((unsigned)count), b(64);
 #define BR(LOGM, K)                                                                                           \
   hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
-                     ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
+                     ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
 #define BRV(V, K, W)                                                                                          \
   hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,          \
-                     p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, (u64)tv, mode, out, ct_v, refreshed, sign)
+                     p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
 #define BR2(K) do { if (ctx->br_variant == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
   if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
@@ -1118,7 +1108,25 @@ int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t
   if (rc) return rc;
   if (count < 0 || (count > 0 && (!d_small || !d_out))) return fail(ctx, FHE_E_ARG, "bad pbs arguments");
   if (count == 0) return FHE_OK;
-  return launch_br(ctx, d_small, count, tv, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+  return launch_br(ctx, d_small, count, BrTv{tv, 0, 0}, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+static int log2i(int x) {
+  int l = 0;
+  while ((1 << l) < x) ++l;
+  return l;
+}
+
+int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t base, uint64_t step,
+                      int32_t log_slots, uint64_t* d_out, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  const int logN = log2i(ctx->p.N);
+  if (count < 0 || (count > 0 && (!d_small || !d_out)) || log_slots < 0 || log_slots > logN)
+    return fail(ctx, FHE_E_ARG, "bad pbs-lut arguments");
+  if (count == 0) return FHE_OK;
+  return launch_br(ctx, d_small, count, BrTv{base, step, logN - log_slots}, 0, d_out, nullptr, nullptr, nullptr,
+                   (hipStream_t)stream);
 }
 
 static int ensure_ws(fhe_ctx* ctx, size_t bytes) {
@@ -1143,11 +1151,72 @@ static int bit_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* 
   for (int i = 0; i < P; ++i) {
     int rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - 1 - i, 1ull << 62, small, st);
     if (rc) return rc;
-    const u64 tv = 1ull << (63 - P + i);
-    rc = launch_br(ctx, small, count, tv, 1, nullptr, d_ct_v, d_ref, (i == P - 1) ? d_sign : nullptr, st);
+    rc = launch_br(ctx, small, count, BrTv{1ull << (63 - P + i), 0, 0}, 1, nullptr, d_ct_v, d_ref,
+                   (i == P - 1) ? d_sign : nullptr, st);
     if (rc) return rc;
   }
   return FHE_OK;
+}
+
+// Sign of the msg_bits-bit value v in d_ct_v (consumed) with 3-bit digits
+// (DESIGN.md §3.4): the low m = P - 3 bits are cleared LSB-first, each full
+// digit [b, b+3) by two bootstraps (its top bit by a sign bootstrap; then,
+// with a zero padding bit, its two low bits by a 4-slot staircase LUT),
+// leftover bits by single-bit rounds; the top digit's MSB is the sign.
+int fhe_sign_pbs_count(int32_t msg_bits) {
+  if (msg_bits < 1) return 0;
+  if (msg_bits < 4) return msg_bits;
+  const int m = msg_bits - 3;
+  return 2 * (m / 3) + m % 3 + 1;
+}
+
+static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
+                        hipStream_t st) {
+  const fhe_params& p = ctx->p;
+  const int P = p.msg_bits, logN = log2i(p.N);
+  int rc;
+  if (P < 4) {
+    for (int i = 0; i < P; ++i) {
+      if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - 1 - i, 1ull << 62, small, st))) return rc;
+      if ((rc = launch_br(ctx, small, count, BrTv{1ull << (63 - P + i), 0, 0}, 1, nullptr, d_ct_v, nullptr,
+                          (i == P - 1) ? d_sign : nullptr, st)))
+        return rc;
+    }
+    return FHE_OK;
+  }
+  const int m = P - 3;
+  int b = 0;
+  for (; b + 3 <= m; b += 3) {
+    // digit MSB (bit b+2): sign bootstrap of v << (P-b-3) centred by 2^60
+    if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 3, 1ull << 60, small, st))) return rc;
+    if ((rc = launch_br(ctx, small, count, BrTv{1ull << (65 - P + b), 0, 0}, 1, nullptr, d_ct_v, nullptr, nullptr,
+                        st)))
+      return rc;
+    // bits b, b+1: top bit is now 0 -> 4-slot staircase, output D' * 2^b * Delta
+    if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 3, 1ull << 60, small, st))) return rc;
+    if ((rc = launch_br(ctx, small, count, BrTv{0, 1ull << (64 - P + b), logN - 2}, 2, nullptr, d_ct_v, nullptr,
+                        nullptr, st)))
+      return rc;
+  }
+  for (; b < m; ++b) {
+    if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 1, 1ull << 62, small, st))) return rc;
+    if ((rc = launch_br(ctx, small, count, BrTv{1ull << (63 - P + b), 0, 0}, 1, nullptr, d_ct_v, nullptr, nullptr,
+                        st)))
+      return rc;
+  }
+  // sign = MSB of the top digit [P-3, P)
+  if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, 0, 1ull << 60, small, st))) return rc;
+  return launch_br(ctx, small, count, BrTv{1ull << 62, 0, 0}, 1, nullptr, d_ct_v, nullptr, d_sign, st);
+}
+
+int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || (count > 0 && (!d_ct_v || !d_sign))) return fail(ctx, FHE_E_ARG, "bad sign arguments");
+  if (count == 0) return FHE_OK;
+  rc = ensure_ws(ctx, 8 * (size_t)count * fhe_small_lwe_words(&ctx->p));
+  if (rc) return rc;
+  return sign_extract(ctx, d_ct_v, count, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream);
 }
 
 int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_refreshed, uint64_t* d_sign,
@@ -1172,14 +1241,13 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   const fhe_params& p = ctx->p;
   hipStream_t st = (hipStream_t)stream;
   const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
-  // workspace: inputs (B*D big) | ct_v (B big) | refreshed (B big) | sign (B big) | small (B) | v (B)
-  const size_t bytes = 8 * ((size_t)B * D * Wb + 3 * (size_t)B * Wb + (size_t)B * Ws + (size_t)B);
+  // workspace: inputs (B*D big) | ct_v (B big) | sign (B big) | small (B) | v (B)
+  const size_t bytes = 8 * ((size_t)B * D * Wb + 2 * (size_t)B * Wb + (size_t)B * Ws + (size_t)B);
   rc = ensure_ws(ctx, bytes);
   if (rc) return rc;
   u64* cin = (u64*)ctx->ws;
   u64* ctv = cin + (size_t)B * D * Wb;
-  u64* ref = ctv + (size_t)B * Wb;
-  u64* sgn = ref + (size_t)B * Wb;
+  u64* sgn = ctv + (size_t)B * Wb;
   u64* small = sgn + (size_t)B * Wb;
   int64_t* v = (int64_t*)(small + (size_t)B * Ws);
   rc = fhe_encrypt_batch(ctx, d_qx, B * D, enc_seed, id0, cin, stream);
@@ -1194,7 +1262,7 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   // computes the encrypted threshold bit [acc < T] exactly.
   rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
   if (rc) return rc;
-  rc = bit_extract(ctx, ctv, B, ref, sgn, small, st);
+  rc = sign_extract(ctx, ctv, B, sgn, small, st);
   if (rc) return rc;
   rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
   if (rc) return rc;

@@ -51,6 +51,9 @@ SIGNATURES = [
     ("fhe_keyswitch_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
     ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
     ("fhe_bit_extract_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp, _vp]),
+    ("fhe_sign_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
+    ("fhe_sign_pbs_count", C.c_int, [_i32]),
+    ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     ("fhe_quantize_pairs", C.c_int, [_CTXP, _vp, _i32, _vp, _i32, _i64, _i32, C.c_double, _i64, _i64, _i64, _vp, _vp]),
     ("fhe_dequantize", C.c_int, [_CTXP, _vp, _i64, C.c_double, _vp, _vp]),

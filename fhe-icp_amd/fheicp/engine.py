@@ -152,6 +152,21 @@ class Engine:
         self._chk(self._L.fhe_pbs_batch(self._ctx, _ptr(small), n, C.c_uint64(tv), _ptr(out), _stream(self.device)))
         return out
 
+    def pbs_lut(self, small: torch.Tensor, base: int, step: int, log_slots: int) -> torch.Tensor:
+        """Staircase bootstrap (fhe_pbs_lut_batch)."""
+        n = small.numel() // self.Ws
+        out = self.empty_big(n)
+        self._chk(self._L.fhe_pbs_lut_batch(self._ctx, _ptr(small), n, C.c_uint64(base), C.c_uint64(step),
+                                            int(log_slots), _ptr(out), _stream(self.device)))
+        return out
+
+    def sign(self, ct_v: torch.Tensor) -> torch.Tensor:
+        """Consumes ct_v; returns the encryption of [v < 0] at 2^63 (fhe_sign_batch)."""
+        n = ct_v.numel() // self.W
+        sign = self.empty_big(n)
+        self._chk(self._L.fhe_sign_batch(self._ctx, _ptr(ct_v), n, _ptr(sign), _stream(self.device)))
+        return sign
+
     def bit_extract(self, ct_v: torch.Tensor):
         """Consumes ct_v; returns (refreshed, sign) ciphertexts."""
         n = ct_v.numel() // self.W
@@ -162,7 +177,7 @@ class Engine:
         return ref, sign
 
     def compare(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc_seed: int, id0: int = 0):
-        """Fused encrypt -> linear -> bit extraction -> decrypt for B pairs.
+        """Fused encrypt -> linear -> decrypt + sign extraction for B pairs.
 
         Returns (acc int64[B], below int64[B])."""
         B, D = q_x.shape

@@ -37,8 +37,21 @@ class SchemeParams:
         return replace(self, msg_bits=int(P))
 
 
-# Bootstrap gadget by message width (checked by noise_report()).
-PBS_GADGETS = ((18, 15, 2), (22, 12, 3), (24, 10, 4), (26, 8, 5), (27, 7, 6))
+# Bootstrap gadget by message width (checked by noise_report()): the widest
+# P each (base_log, level) supports with >= 9.2 sigma at the decision margin
+# of the 3-bit digit sign extraction (fhe_sign_batch), whose worst round is
+# the low-bits bootstrap of the first digit: margin 2^-4, the first bootstrap's
+# noise amplified by 2^(P-3). The single-bit extraction (fhe_bit_extract_batch:
+# margin 2^-2, amplification 2^(P-2)) is looser at every entry.
+PBS_GADGETS = ((17, 15, 2), (21, 12, 3), (23, 10, 4), (25, 8, 5), (26, 7, 6), (27, 6, 7))
+
+
+def sign_pbs_count(P: int) -> int:
+    """Key switches + bootstraps per sign extraction (fhe_sign_pbs_count)."""
+    if P < 4:
+        return max(P, 0)
+    m = P - 3
+    return 2 * (m // 3) + m % 3 + 1
 
 
 def params_for_bits(P: int) -> SchemeParams:
@@ -58,12 +71,18 @@ def _tuniform_var(b: int) -> float:
     return (2.0 ** (2 * b + 1) + 1.0) / 6.0
 
 
-def noise_report(p: SchemeParams) -> dict:
-    """Variance model (relative to the 2^64 torus) of one bit-extraction round.
+def noise_report(p: SchemeParams, method: str = "digits") -> dict:
+    """Variance model (relative to the 2^64 torus) of the worst extraction round.
 
-    Worst round is i = 1, where the PBS output noise of bit 0 is amplified by
-    2^(P-2) before the sign bootstrap reads it.
+    method "bits" (fhe_bit_extract_batch): round i = 1, the PBS output noise of
+    bit 0 amplified by 2^(P-2), decision margin 1/4 of the torus.
+    method "digits" (fhe_sign_batch, P >= 4): the low-bits bootstrap of the
+    first 3-bit digit, the digit-MSB bootstrap's noise amplified by 2^(P-3),
+    margin 1/16.
     """
+    if method not in ("bits", "digits"):
+        raise ValueError(method)
+    digits = method == "digits" and p.msg_bits >= 4
     q2 = 2.0 ** 128
     s2_bsk = _tuniform_var(p.glwe_noise_bits) / q2
     s2_ksk = _tuniform_var(p.lwe_noise_bits) / q2
@@ -76,16 +95,16 @@ def noise_report(p: SchemeParams) -> dict:
     v_ks = p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk
     v_ks += p.k * p.N / 2 * (2.0 ** (-2 * p.ks_level * p.ks_base_log)) / 12.0
     v_ms = (p.n / 2 + 1) / 12.0 / (2.0 * p.N) ** 2
-    v_amp = v_pbs * 4.0 ** (p.msg_bits - 2)
+    v_amp = v_pbs * 4.0 ** (p.msg_bits - (3 if digits else 2))
     v_total = v_amp + v_ks + v_ms
     sigma = math.sqrt(v_total)
-    margin_sigmas = 0.25 / sigma
+    margin_sigmas = (0.0625 if digits else 0.25) / sigma
     return {
         "log2_sigma_pbs": 0.5 * math.log2(v_pbs),
         "log2_sigma_ks": 0.5 * math.log2(v_ks),
         "log2_sigma_ms": 0.5 * math.log2(v_ms),
         "log2_sigma_total": math.log2(sigma),
         "margin_sigmas": margin_sigmas,
-        # two-sided Gaussian tail at the 1/4-torus decision margin
+        # two-sided Gaussian tail at the decision margin
         "log2_pfail_per_pbs": math.log2(max(math.erfc(margin_sigmas / math.sqrt(2)), 1e-300)),
     }

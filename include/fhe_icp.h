@@ -125,13 +125,26 @@ int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t
 int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_refreshed, uint64_t* d_sign,
                           void* stream);
 
+/* Sign of the msg_bits-bit value v in d_ct_v (consumed): d_sign receives the
+ * encryption of [v < 0] at 2^63 (decrypt with fhe_decrypt_bits_batch). Uses
+ * fhe_sign_pbs_count(msg_bits) key switches + bootstraps per ciphertext:
+ * 3-bit digits, two bootstraps each, 10 at msg_bits = 16. */
+int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, void* stream);
+int fhe_sign_pbs_count(int32_t msg_bits);
+/* Bootstrap with a staircase test vector over 2^log_slots slots of the half
+ * torus: output phase ~ base + floor(phase * 2^log_slots / 2^63) * step for an
+ * input phase in [0, 2^63) (negacyclic beyond). log_slots = 0, step = 0 is
+ * fhe_pbs_batch with tv = base. */
+int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t base, uint64_t step,
+                      int32_t log_slots, uint64_t* d_out, void* stream);
+
 /* ---- fused compare / search ------------------------------------------------
  * One call per batch of B (query, document) pairs — the batched replacement
  * of the per-document loop at batch_operations.py:268-279 and of
  * compare_encrypted (batch_operations.py:206-238):
  *   encrypt q_x (B x D) -> linear with d_w and cst - T -> decrypt the
- *   leveled accumulator -> bit extraction (msg_bits KS + PBS) -> decrypt the
- *   sign bit. d_acc[b] = the decrypted accumulator (exact int64, = Concrete's
+ *   leveled accumulator -> sign extraction (fhe_sign_pbs_count(msg_bits)
+ *   KS + PBS) -> decrypt the sign bit. d_acc[b] = the decrypted accumulator (exact int64, = Concrete's
  *   q_x @ q_w - zp*sum(q_w) + q_b; read from the leveled ciphertext like the
  *   reference's leveled circuit), d_below[b] = 1 iff acc < T (the decrypted
  *   bootstrapped threshold bit; acc >= T <=> score >= min_similarity).

@@ -346,9 +346,17 @@ static uint32_t modswitch(uint64_t a, int log2N2) {
   return (uint32_t)((((a >> (63 - log2N2)) + 1) >> 1) & ((1ull << log2N2) - 1));
 }
 
-/* Bootstrap one small LWE (dim n) with the constant test vector tv; sample
- * extract coefficient 0. out: kN + 1 words under s_big. */
-static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small, uint64_t tv, uint64_t* out,
+/* Test vector TV_j = base + (j >> shift) * step, j in [0, N), extended
+ * negacyclically (a staircase; step 0 = constant). */
+typedef struct { uint64_t base, step; int shift; } tv_desc;
+static uint64_t tv_at(const tv_desc* tv, uint32_t idx, int N) {
+  const uint64_t v = tv->base + (uint64_t)((idx & (uint32_t)(N - 1)) >> tv->shift) * tv->step;
+  return idx < (uint32_t)N ? v : (uint64_t)0 - v;
+}
+
+/* Bootstrap one small LWE (dim n) with test vector tv; sample extract
+ * coefficient 0. out: kN + 1 words under s_big. */
+static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small, const tv_desc* tv, uint64_t* out,
                  uint64_t* work) {
   const int n = P->n, k = P->k, N = P->N, L = P->pbs_level, R = rows(P), bl = P->pbs_base_log;
   const int lg = ilog2(2 * N);
@@ -360,7 +368,7 @@ static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small
   for (int t = 0; t < k * N; ++t) acc[t] = 0;
   for (int t = 0; t < N; ++t) {
     const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
-    acc[(size_t)k * N + t] = idx < (uint32_t)N ? tv : (uint64_t)0 - tv;
+    acc[(size_t)k * N + t] = tv_at(tv, idx, N);
   }
   for (int i = 0; i < n; ++i) {
     const uint32_t ai = modswitch(small[i], lg);
@@ -398,9 +406,25 @@ void ref_pbs_const(const ref_params* P, const uint64_t* bsk, const uint64_t* sma
 #pragma omp parallel
   {
     uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+    const tv_desc d = {tv, 0, 0};
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c)
-      pbs1(P, bsk, small + (size_t)c * (P->n + 1), tv, out + (size_t)c * (P->k * P->N + 1), work);
+      pbs1(P, bsk, small + (size_t)c * (P->n + 1), &d, out + (size_t)c * (P->k * P->N + 1), work);
+    free(work);
+  }
+}
+
+/* Bootstrap with a staircase test vector over 2^log_slots slots of the half
+ * torus (fhe_pbs_lut_batch semantics). */
+void ref_pbs_lut(const ref_params* P, const uint64_t* bsk, const uint64_t* small, int64_t count, uint64_t base,
+                 uint64_t step, int log_slots, uint64_t* out) {
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+    const tv_desc d = {base, step, ilog2(P->N) - log_slots};
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c)
+      pbs1(P, bsk, small + (size_t)c * (P->n + 1), &d, out + (size_t)c * (P->k * P->N + 1), work);
     free(work);
   }
 }
@@ -438,7 +462,8 @@ void ref_bit_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* k
         sh[Wb - 1] += 1ull << 62;
         keyswitch1(P, ksk, sh, sm);
         const uint64_t tv = 1ull << (63 - Pb + i);
-        pbs1(P, bsk, sm, tv, ob, work);
+        const tv_desc d = {tv, 0, 0};
+        pbs1(P, bsk, sm, &d, ob, work);
         for (int t = 0; t < Wb - 1; ++t) ob[t] = (uint64_t)0 - ob[t];
         ob[Wb - 1] = tv - ob[Wb - 1];
         for (int t = 0; t < Wb; ++t) { cv[t] -= ob[t]; acc[t] += ob[t]; }
@@ -447,6 +472,75 @@ void ref_bit_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* k
     }
     free(work); free(sh); free(sm); free(ob);
   }
+}
+
+/* ------------------------------------------------------------ sign ----- */
+/* One round on ct_v: sh = (ct_v << shift) + add on the body, KS, PBS with tv;
+ * mode 1: d = trivial(tv.base) - PBS; mode 2: d = PBS; then ct_v -= d. */
+static void sign_round(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* cv, int shift,
+                       uint64_t add, const tv_desc* tv, int mode, uint64_t* sh, uint64_t* sm, uint64_t* ob,
+                       uint64_t* work) {
+  const int Wb = P->k * P->N + 1;
+  for (int t = 0; t < Wb; ++t) sh[t] = cv[t] << shift;
+  sh[Wb - 1] += add;
+  keyswitch1(P, ksk, sh, sm);
+  pbs1(P, bsk, sm, tv, ob, work);
+  if (mode == 1) {
+    for (int t = 0; t < Wb - 1; ++t) ob[t] = (uint64_t)0 - ob[t];
+    ob[Wb - 1] = tv->base - ob[Wb - 1];
+  }
+  for (int t = 0; t < Wb; ++t) cv[t] -= ob[t];
+}
+
+/* Sign of the P-bit value in ct_v with 3-bit digits (the
+ * algorithm of fhe_sign_batch): clear the low m = P - 3 bits LSB-first, a
+ * full digit [b, b+3) by a sign bootstrap of its top bit (v << (P-b-3),
+ * centred by 2^60, tv 2^(65-P+b)) then a 4-slot staircase of its two low bits
+ * (step 2^(64-P+b)); leftover bits by single-bit rounds; then the top digit's
+ * MSB. sign[count x (kN+1)] encrypts [v < 0] at 2^63; ct_v is consumed. */
+void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
+                      uint64_t* sign) {
+  const int Wb = P->k * P->N + 1, Pb = P->msg_bits, lgN = ilog2(P->N);
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+    uint64_t* sh = (uint64_t*)malloc(8 * (size_t)Wb);
+    uint64_t* sm = (uint64_t*)malloc(8 * (size_t)(P->n + 1));
+    uint64_t* ob = (uint64_t*)malloc(8 * (size_t)Wb);
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c) {
+      uint64_t* cv = ct_v + (size_t)c * Wb;
+      if (Pb < 4) {
+        for (int i = 0; i < Pb; ++i) {
+          const tv_desc d = {1ull << (63 - Pb + i), 0, 0};
+          sign_round(P, bsk, ksk, cv, Pb - 1 - i, 1ull << 62, &d, 1, sh, sm, ob, work);
+        }
+      } else {
+        const int m = Pb - 3;
+        int b = 0;
+        for (; b + 3 <= m; b += 3) {
+          const tv_desc hi = {1ull << (65 - Pb + b), 0, 0};
+          sign_round(P, bsk, ksk, cv, Pb - b - 3, 1ull << 60, &hi, 1, sh, sm, ob, work);
+          const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - 2};
+          sign_round(P, bsk, ksk, cv, Pb - b - 3, 1ull << 60, &lo, 2, sh, sm, ob, work);
+        }
+        for (; b < m; ++b) {
+          const tv_desc d = {1ull << (63 - Pb + b), 0, 0};
+          sign_round(P, bsk, ksk, cv, Pb - b - 1, 1ull << 62, &d, 1, sh, sm, ob, work);
+        }
+        const tv_desc top = {1ull << 62, 0, 0};
+        sign_round(P, bsk, ksk, cv, 0, 1ull << 60, &top, 1, sh, sm, ob, work);
+      }
+      memcpy(sign + (size_t)c * Wb, ob, 8 * (size_t)Wb);
+    }
+    free(work); free(sh); free(sm); free(ob);
+  }
+}
+
+int ref_sign_pbs_count(int Pb) {
+  if (Pb < 1) return 0;
+  if (Pb < 4) return Pb;
+  return 2 * ((Pb - 3) / 3) + (Pb - 3) % 3 + 1;
 }
 
 /* Decrypt the sign ciphertext: 1 iff phase in [2^62, 3*2^62) i.e. bit set. */

@@ -55,6 +55,9 @@ def lib():
         L.ref_modswitch.argtypes = [P, u64p, C.c_int64, u32p]
         L.ref_pbs_const.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, u64p]
         L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
+        L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
+        L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_pbs_count.argtypes = [C.c_int]; L.ref_sign_pbs_count.restype = C.c_int
         L.ref_negacyclic_mul.argtypes = [u64p, u64p, u64p, C.c_int]
         L.ref_decompose.argtypes = [C.c_uint64, C.c_int, C.c_int, i64p]
         L.ref_tuniform.argtypes = [C.c_uint64, C.c_int]; L.ref_tuniform.restype = C.c_int64
@@ -160,6 +163,22 @@ class RefTFHE:
         lib().ref_pbs_const(C.byref(self.P), u64(self.bsk), u64(small), cnt, C.c_uint64(tv), u64(out))
         return out
 
+    def pbs_lut(self, small: np.ndarray, base: int, step: int, log_slots: int) -> np.ndarray:
+        small = np.ascontiguousarray(small, dtype=np.uint64)
+        cnt = small.size // (self.n + 1)
+        out = np.zeros((cnt, self.big + 1), np.uint64)
+        lib().ref_pbs_lut(C.byref(self.P), u64(self.bsk), u64(small), cnt, C.c_uint64(base), C.c_uint64(step),
+                          int(log_slots), u64(out))
+        return out
+
+    def sign_extract(self, ct_v: np.ndarray) -> np.ndarray:
+        """fhe_sign_batch restated: encryption of [v < 0] at 2^63 (ct_v copied)."""
+        cv = np.array(ct_v, dtype=np.uint64, copy=True, order="C")
+        cnt = cv.size // (self.big + 1)
+        sign = np.zeros((cnt, self.big + 1), np.uint64)
+        lib().ref_sign_extract(C.byref(self.P), u64(self.bsk), u64(self.ksk), u64(cv), cnt, u64(sign))
+        return sign
+
     def bit_extract(self, ct_v: np.ndarray):
         cv = np.array(ct_v, dtype=np.uint64, copy=True, order="C")
         cnt = cv.size // (self.big + 1)
@@ -195,3 +214,5 @@ def chacha20_block(key_words, counter: int, nonce_words) -> np.ndarray:
     return out
 
 
+def sign_pbs_count(P: int) -> int:
+    return int(lib().ref_sign_pbs_count(int(P)))

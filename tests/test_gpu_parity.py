@@ -184,3 +184,48 @@ def test_bit_extract_real_params_v3_kernel(need_gpu, oracle_lib, monkeypatch):
     ref_ct, sign = eng.bit_extract(eng.encrypt(v, seed=22))
     assert np.array_equal(eng.decrypt(ref_ct).cpu().numpy(), v)
     assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+
+
+def test_sign_toy_all_values_vs_oracle(toy):
+    """Digit sign extraction (fhe_sign_batch): every toy value, and the GPU
+    sign ciphertexts' phases track the oracle's restatement."""
+    eng, ref = toy
+    P = eng.msg_bits
+    v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
+    sign = eng.sign(eng.encrypt(v, seed=41))
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    sel = np.array([0, 1, 127, 128, 129, 255])
+    s_ref = ref.sign_extract(ref.encrypt_ints(v[sel], seed=41, id0=0))
+    assert np.array_equal(ref.decrypt_bits(s_ref), (v[sel] < 0).astype(np.int64))
+    d = signed(u64(eng.phase(sign[sel].contiguous())) - ref.phase(s_ref))
+    assert np.abs(d).max() < 2 ** 56
+
+
+@pytest.mark.parametrize("P", [16, 21])
+def test_sign_real_params(need_gpu, P):
+    """Real parameters at the C2/C4 (P=16) and C3 (P=21) widths, boundaries included."""
+    eng = Engine(params_for_bits(P), 0)
+    eng.keygen(900 + P)
+    rng = np.random.default_rng(P)
+    h = 2 ** (P - 1)
+    v = rng.integers(-h, h, 1024)
+    v[:8] = [-h, -h + 1, -2, -1, 0, 1, h - 2, h - 1]
+    sign = eng.sign(eng.encrypt(v, seed=P))
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    eng.close()
+
+
+def test_pbs_lut_real_vs_oracle(real):
+    """4-slot staircase bootstrap on the real parameters, against the oracle."""
+    eng, ref = real
+    D = np.array([0, 1, 2, 3], dtype=np.uint64)
+    msg = (D << np.uint64(61)) + np.uint64(1 << 60)
+    ct = eng.to_dev(msg.view(np.int64))
+    enc = eng.encrypt(np.zeros(4, np.int64), seed=51)        # encryptions of 0 ...
+    enc[:, -1] += ct                                          # ... shifted to the raw phases
+    small = eng.keyswitch(enc, 0, 0)
+    out = eng.pbs_lut(small, 0, 1 << 48, 2)
+    out_ref = ref.pbs_lut(u64(small), 0, 1 << 48, 2)
+    ph = signed(u64(eng.phase(out)))
+    assert np.abs(ph - signed(ref.phase(out_ref))).max() < 2 ** 46
+    assert np.abs(ph - (D.astype(np.int64) << 48)).max() < 2 ** 46

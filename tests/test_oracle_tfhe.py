@@ -125,3 +125,29 @@ def test_real_params_roundtrip(oracle_lib):
     sm = ref.keyswitch(ct)
     err = ref.phase(sm, small=True).view(np.int64) - (v << 48)
     assert np.abs(err).max() < 2 ** 58
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8])
+def test_sign_extract_digits_all_values(toy_ref, P):
+    """The 3-bit digit sign algorithm (fhe_sign_batch) on every P-bit value,
+    covering each branch shape: P < 4, full digits, leftover single bits."""
+    r = toy_ref.with_msg_bits(P)
+    v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
+    sign = r.sign_extract(r.encrypt_ints(v, seed=100 + P))
+    assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
+
+
+def test_sign_pbs_count(oracle_lib):
+    from oracle.tfhe_ref import sign_pbs_count
+    want = {1: 1, 2: 2, 3: 3, 4: 2, 6: 3, 7: 4, 8: 5, 9: 5, 16: 10, 21: 13, 26: 17}
+    assert {P: sign_pbs_count(P) for P in want} == want
+
+
+def test_pbs_lut_staircase(toy_ref):
+    """4-slot staircase bootstrap: phase D*2^61 + 2^60 -> D * step."""
+    D = np.array([0, 1, 2, 3, 3, 2, 1, 0], dtype=np.uint64)
+    msg = (D << np.uint64(61)) + np.uint64(1 << 60)
+    sm = toy_ref.keyswitch(toy_ref.encrypt_raw(msg, seed=11))
+    out = toy_ref.pbs_lut(sm, 0, 1 << 50, 2)
+    err = toy_ref.phase(out).view(np.int64) - (D.astype(np.int64) << 50)
+    assert np.abs(err).max() < 2 ** 45

@@ -8,7 +8,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from fheicp.params import PBS_GADGETS, params_for_bits, noise_report
+from fheicp.params import PBS_GADGETS, params_for_bits, noise_report, sign_pbs_count
 from fheicp.search import sharded_topk
 
 
@@ -16,10 +16,21 @@ from fheicp.search import sharded_topk
 def test_gadget_table_has_margin(pmax, beta, lvl):
     p = params_for_bits(pmax)
     assert (p.pbs_base_log, p.pbs_level) == (beta, lvl)
-    r = noise_report(p)
-    # >= 9.2 sigma at the 1/4-torus decision margin  <=>  p_fail <= 2^-64 per PBS
-    assert r["margin_sigmas"] > 9.2, r
-    assert r["log2_pfail_per_pbs"] < -64
+    # >= 9.2 sigma at the decision margin  <=>  p_fail <= 2^-64 per PBS, for
+    # the digit sign extraction (1/16 margin) and the single-bit one (1/4)
+    for method in ("digits", "bits"):
+        r = noise_report(p, method)
+        assert r["margin_sigmas"] > 9.2, (method, r)
+        assert r["log2_pfail_per_pbs"] < -64
+    # and the next width up would not be (the table is tight)
+    if pmax < 27:
+        assert noise_report(p.with_msg_bits(pmax + 1))["margin_sigmas"] < 9.2
+
+
+def test_sign_pbs_count_matches_oracle(oracle_lib):
+    for P in range(1, 28):
+        assert sign_pbs_count(P) == oracle_lib.sign_pbs_count(P)
+    assert sign_pbs_count(16) == 10
 
 
 def test_params_for_bits_limits():
