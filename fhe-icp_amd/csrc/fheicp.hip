@@ -24,6 +24,7 @@
 #include "wave_fft.h"
 #include "br_m512.h"
 #include "br_m512q.h"
+#include "br_v4.h"
 
 using namespace fhei;
 typedef uint64_t u64;
@@ -655,6 +656,227 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
   if (tid == 0) br_emit(mode, acc[K * N], true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
 }
 
+// ---- blind rotation v4 (br_v4.h): a wave per GLWE component ---------------
+// BSK conversion: one wave per polynomial, stored [poly][u][lane] (layout LD
+// of the forward transform) and scaled by 1/M.
+__global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bsk, int npoly,
+                                                      const c64* __restrict__ tw, const c64* __restrict__ twist,
+                                                      c64* __restrict__ out) {
+  using namespace v4;
+  __shared__ c64 twl[NTW * 64];
+  __shared__ c64 twt[S * 64];
+  __shared__ c64 scr[SCR];
+  const int lane = threadIdx.x;
+  fill_tables(twl, twt, tw, twist, lane, 64);
+  __syncthreads();
+  const double inv = 1.0 / (double)M;
+  for (int poly = blockIdx.x; poly < npoly; poly += gridDim.x) {
+    const u64* src = bsk + (size_t)poly * N;
+    c64 v[S];
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const int t = u * 64 + lane;
+      v[u] = cmul({(double)(int64_t)src[t], (double)(int64_t)src[t + M]}, twt[t]);
+    }
+    forward(v, twl, scr, lane);
+    c64* dst = out + (size_t)poly * M;
+#pragma unroll
+    for (int u = 0; u < S; ++u) dst[u * 64 + lane] = {v[u].x * inv, v[u].y * inv};
+  }
+}
+
+// Balanced gadget digits of x (level 0 = most significant) into d[0..L).
+template <int L, bool A32>
+__device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int beta, int (&d)[L]) {
+  const int prec = L * beta;
+  if constexpr (A32) {
+    uint32_t r = ((x >> (31 - prec)) + 1) >> 1;
+    const uint32_t B = 1u << beta, hb = B >> 1;
+#pragma unroll
+    for (int l = L - 1; l >= 0; --l) {
+      const uint32_t dd = r & (B - 1);
+      r >>= beta;
+      const uint32_t cy = dd >= hb;
+      d[l] = (int)dd - (int)(cy << beta);
+      r += cy;
+    }
+  } else {
+    u64 r = ((x >> (63 - prec)) + 1) >> 1;
+    const u64 B = 1ull << beta, hb = B >> 1;
+#pragma unroll
+    for (int l = L - 1; l >= 0; --l) {
+      const u64 dd = r & (B - 1);
+      r >>= beta;
+      const u64 cy = dd >= hb;
+      d[l] = (int)dd - (int)(cy << beta);
+      r += cy;
+    }
+  }
+}
+
+// DBG != 0 only for timing experiments (tools/prof_br.py, FHEICP_V4_DBG):
+// 1 twiddles from a register, 2 no BSK loads, 4 no barriers, 8 no FFT
+// relayout, 16 no LDS rotation, 32 no LDS reads of the other components.
+template <int L, bool A32, int DBG = 0>
+__global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
+                                                              int beta, const c64* __restrict__ bsk,
+                                                              const c64* __restrict__ tw,
+                                                              const c64* __restrict__ twist, BrTv tv, int mode,
+                                                              u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                              u64* __restrict__ refreshed, u64* __restrict__ sign) {
+  using namespace v4;
+  using AT = Acc<A32>;
+  using T = typename AT::T;
+  __shared__ c64 xbuf[G * WPC * SCR];  // one 8.5 KB slot per wave
+  __shared__ c64 twl[NTW * 64];
+  __shared__ c64 twt[S * 64];
+  __shared__ uint16_t atab[G][NMAX + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w / WPC, comp = w - g * WPC;
+  const int64_t c = (int64_t)blockIdx.x * G + g;
+  c64* slot = xbuf + (g * WPC + comp) * SCR;
+  const c64* ctslots = xbuf + g * WPC * SCR;
+  T* sa = reinterpret_cast<T*>(slot);
+
+  fill_tables(twl, twt, tw, twist, tid, NT);
+  for (int x = tid; x < G * (n + 1); x += NT) {
+    const int gg = x / (n + 1), ii = x - gg * (n + 1);
+    const int64_t cc = (int64_t)blockIdx.x * G + gg;
+    atab[gg][ii] = cc < count ? (uint16_t)modswitch_2n(small[(size_t)cc * (n + 1) + ii], 11) : (uint16_t)0;
+  }
+  __syncthreads();
+
+  T acc[2 * S];
+  {
+    const uint32_t bt = atab[g][n];
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t idx = (uint32_t)(s * 64 + lane + bt) & (2 * N - 1);
+      acc[s] = comp == K ? AT::from64(tv_rot(tv, idx, N)) : (T)0;
+    }
+  }
+
+  constexpr int R = WPC * L;
+  const c64 wf = {0.5 + (double)beta * 1e-3, (double)L * 1e-3};  // DBG stand-in value
+  for (int i = 0; i < n; ++i) {
+    const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)atab[g][i]);
+    // X^a ACC - ACC through the wave's slot, then the gadget digits
+    if constexpr ((DBG & 16) == 0) {
+#pragma unroll
+      for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    c64 v[S];
+    uint32_t dg[L > 1 ? L - 1 : 1][S];  // levels >= 1, two int16 digits per word
+    T rot[2 * S];  // all 16 rotated words as one batch of LDS reads
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t src = (uint32_t)(s * 64 + lane - (int)a) & (2 * N - 1);
+      rot[s] = (DBG & 16) ? acc[(s + 1) & 15] + (T)src : sa[src & (N - 1)];
+    }
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t src = (uint32_t)(s * 64 + lane - (int)a) & (2 * N - 1);
+      T r = rot[s];
+      if (src >= (uint32_t)N) r = (T)0 - r;
+      int d[L];
+      decompose_v4<L, A32>((T)(r - acc[s]), beta, d);
+#pragma unroll
+      for (int l = 1; l < L; ++l) {
+        if (s < S) dg[l - 1][s] = (uint32_t)(d[l] & 0xffff);
+        else dg[l - 1][s - S] |= (uint32_t)d[l] << 16;
+      }
+      if (s < S) v[s].x = (double)d[0];
+      else v[s - S].y = (double)d[0];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    c64 mac[S];
+#pragma unroll
+    for (int u = 0; u < S; ++u) mac[u] = {0.0, 0.0};
+    const c64* Gi = bsk + (size_t)i * R * WPC * M;
+#pragma unroll
+    for (int lv = 0; lv < L; ++lv) {
+      if (lv > 0) {
+#pragma unroll
+        for (int u = 0; u < S; ++u)
+          v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+      }
+      {
+        c64 tws[S];
+#pragma unroll
+        for (int u = 0; u < S; ++u) tws[u] = twt[u * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < S; ++u) v[u] = cmul(v[u], tws[u]);
+      }
+      // own-component BSK row: loads fly during the transform
+      c64 kb[S];
+      {
+        const c64* gp = Gi + ((size_t)(comp * L + lv) * WPC + comp) * M;
+#pragma unroll
+        for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gp[u * 64 + lane];
+      }
+      forward<DBG>(v, twl, slot, lane, wf);
+#pragma unroll
+      for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
+      // own component first (no other wave needed), then the two other rows'
+      // BSK loads fly across the barrier
+#pragma unroll
+      for (int u = 0; u < S; ++u) cmac(mac[u], v[u], kb[u]);
+      c64 kx[K][S];
+#pragma unroll
+      for (int ci = 0; ci < K; ++ci) {
+        const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
+        const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
+#pragma unroll
+        for (int u = 0; u < S; ++u) kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
+      }
+      if constexpr ((DBG & 4) == 0) lds_barrier();
+#pragma unroll
+      for (int ci = 0; ci < K; ++ci) {
+        const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
+        const c64* fs = ctslots + cin * SCR;
+        c64 fv[S];
+#pragma unroll
+        for (int u = 0; u < S; ++u) fv[u] = (DBG & 32) ? v[u] : fs[u * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < S; ++u) cmac(mac[u], fv[u], kx[ci][u]);
+      }
+      if constexpr ((DBG & 4) == 0) lds_barrier();
+    }
+    inverse<DBG>(mac, twl, slot, lane, wf);
+    c64 tws[S];
+#pragma unroll
+    for (int u = 0; u < S; ++u) tws[u] = twt[u * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const c64 z = cmulc(mac[u], tws[u]);
+      acc[u] += AT::from_f64(z.x);
+      acc[u + S] += AT::from_f64(z.y);
+    }
+  }
+
+  // sample extraction of coefficient 0: mask word t of component comp < K
+  // is -ACC[N - t] (t > 0), read reversed through the slot
+#pragma unroll
+  for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (c < count) {
+    const int W = K * N + 1;
+    if (comp < K) {
+#pragma unroll
+      for (int s = 0; s < 2 * S; ++s) {
+        const int t = s * 64 + lane;
+        const u64 x = t == 0 ? AT::to64(sa[0]) : (u64)0 - AT::to64(sa[N - t]);
+        br_emit(mode, x, false, tv, (size_t)c * W + comp * N + t, out, ct_v, refreshed, sign);
+      }
+    } else if (lane == 0) {
+      br_emit(mode, AT::to64(acc[0]), true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
+    }
+  }
+}
+
 // acc_out[b] = v[b] + T
 __global__ void k_add_scalar(const int64_t* __restrict__ v, int64_t B, int64_t T, int64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -742,7 +964,8 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
   bool prof = false;
   ProfAcc prof_br, prof_ks;
-  int br_variant = 2;  // N=1024 blind rotation: 2 = two waves/ct (default), 3 = four waves/ct
+  int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2, 3
+  int v4_dbg = 0;      // timing experiments only (FHEICP_V4_DBG), wrong results
 };
 
 static std::mutex g_err_mu;
@@ -815,7 +1038,15 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   fhe_ctx* ctx = new fhe_ctx();
   ctx->p = *params;
   ctx->device = device;
-  if (const char* e = getenv("FHEICP_BR_VARIANT")) ctx->br_variant = atoi(e) == 3 ? 3 : 2;
+  if (const char* e = getenv("FHEICP_BR_VARIANT")) {
+    const int v = atoi(e);
+    ctx->br_variant = (v == 2 || v == 3 || v == 4) ? v : 4;
+  }
+  if (const char* e = getenv("FHEICP_V4_DBG")) ctx->v4_dbg = atoi(e);
+  // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
+  if (ctx->br_variant == 4 && !(params->k == 2 && params->n <= v4::NMAX && params->pbs_level <= 7 &&
+                                 (params->pbs_level == 1 || params->pbs_base_log <= 16)))
+    ctx->br_variant = 2;
   if (device >= 0) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
@@ -912,7 +1143,10 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
     case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
     case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
     case 1024:
-      if (ctx->br_variant == 3)
+      if (ctx->br_variant == 4)
+        hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw,
+                           ctx->twist, ctx->bsk_fft);
+      else if (ctx->br_variant == 3)
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
       else
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
@@ -1087,7 +1321,39 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,          \
                      p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
 #define BR2(K) do { if (ctx->br_variant == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
-  if (p.N == 256 && p.k == 1) BR(7, 1);
+#define BR4(L, A32)                                                                                           \
+  hipLaunchKernelGGL((k_blind_rotate_v4<L, A32>), dim3((unsigned)((count + v4::G - 1) / v4::G)), dim3(v4::NT), 0, \
+                     st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, \
+                     refreshed, sign)
+#define BR4D(D)                                                                                               \
+  hipLaunchKernelGGL((k_blind_rotate_v4<2, true, D>), dim3((unsigned)((count + v4::G - 1) / v4::G)), dim3(v4::NT), \
+                     0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out,     \
+                     ct_v, refreshed, sign)
+  if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
+      p.pbs_level * p.pbs_base_log <= 31) {
+    switch (ctx->v4_dbg) {
+      case 1: BR4D(1); break;
+      case 2: BR4D(2); break;
+      case 4: BR4D(4); break;
+      case 8: BR4D(8); break;
+      case 16: BR4D(16); break;
+      case 32: BR4D(32); break;
+      case 6: BR4D(6); break;
+      default: BR4D(63); break;
+    }
+  } else if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4) {
+    const bool a32 = p.pbs_level * p.pbs_base_log <= 31;
+    switch (p.pbs_level) {
+      case 1: if (a32) BR4(1, true); else BR4(1, false); break;
+      case 2: if (a32) BR4(2, true); else BR4(2, false); break;
+      case 3: BR4(3, false); break;
+      case 4: BR4(4, false); break;
+      case 5: BR4(5, false); break;
+      case 6: BR4(6, false); break;
+      case 7: BR4(7, false); break;
+      default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: pbs_level > 7");
+    }
+  } else if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
   else if (p.N == 512 && p.k == 1) BR(8, 1);
   else if (p.N == 512 && p.k == 2) BR(8, 2);
@@ -1097,6 +1363,8 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   else return fail(ctx, FHE_E_ARG, "unsupported (N, k)");
 #undef BR
 #undef BR2
+#undef BR4
+#undef BR4D
 #undef BRV
   prof_end(ctx, ctx->prof_br, st, e1, count);
   HIPCHK(ctx, hipGetLastError());

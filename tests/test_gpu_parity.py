@@ -174,9 +174,11 @@ def test_topk_matches_stable_sort(need_gpu):
         assert np.all(got_i[len(exp):] == -1)
 
 
-def test_bit_extract_real_params_v3_kernel(need_gpu, oracle_lib, monkeypatch):
-    """The 4-wave blind rotation (FHEICP_BR_VARIANT=3) gives the same results."""
-    monkeypatch.setenv("FHEICP_BR_VARIANT", "3")
+@pytest.mark.parametrize("variant", ["2", "3"])
+def test_bit_extract_real_params_other_kernels(need_gpu, oracle_lib, monkeypatch, variant):
+    """The A/B blind-rotation kernels (FHEICP_BR_VARIANT=2: two waves per
+    ciphertext, 3: four) give the same results as the default (v4)."""
+    monkeypatch.setenv("FHEICP_BR_VARIANT", variant)
     eng = Engine(REAL16, 0)
     eng.keygen(777)
     P = eng.msg_bits

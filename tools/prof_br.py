@@ -18,11 +18,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=1024)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--P", type=int, default=16)
-ap.add_argument("--variants", default="2,3")
+ap.add_argument("--variants", default="4,2")
+ap.add_argument("--dbg", default="", help="comma list of FHEICP_V4_DBG values to time (v4 only; wrong results)")
 a = ap.parse_args()
 import os
-for var in a.variants.split(","):
+runs = [(v, "0") for v in a.variants.split(",")] + [("4", d) for d in a.dbg.split(",") if d]
+for var, dbg in runs:
     os.environ["FHEICP_BR_VARIANT"] = var
+    os.environ["FHEICP_V4_DBG"] = dbg
     eng = Engine(params_for_bits(a.P), 0)
     eng.keygen(7)
     v = np.random.default_rng(1).integers(-(2 ** (a.P - 1)), 2 ** (a.P - 1), a.B)
@@ -34,6 +37,6 @@ for var in a.variants.split(","):
     torch.cuda.synchronize()
     br = eng.profile_read("blind_rotate")
     ks = eng.profile_read("keyswitch")
-    print(f"variant={var} B={a.B} blind_rotate {br['total_ms'] / br['launches']:.3f} ms/launch "
+    print(f"variant={var} dbg={dbg} B={a.B} blind_rotate {br['total_ms'] / br['launches']:.3f} ms/launch "
           f"({a.B * br['launches'] / br['total_ms'] * 1e3:.0f} PBS/s), keyswitch {ks['total_ms'] / ks['launches']:.3f} ms/launch")
     eng.close()
