@@ -5,19 +5,16 @@
 // cross-wave LDS relayout (two barriers) per transform — 18 barriers per
 // step — and leaves 2 waves per SIMD. Here a wave owns whole transforms
 // (8 complex values per lane, S = 8): the 9 index bits live in 3 slot bits
-// and 6 lane bits, and a transform needs three v_permlane swaps plus ONE
-// relayout through the wave's own LDS slot (no barrier). The waves of a
+// and 6 lane bits; a transform is three radix-8 passes joined by two
+// relayouts through the wave's own LDS slot (no barrier). The waves of a
 // ciphertext meet only in the external product: each writes the FFT of its
 // component's digit polynomial to LDS, and wave c accumulates output
 // component c from all three (2 barriers per gadget level, 4 per step).
 // 6 waves x 2 workgroups per CU = 3 waves per SIMD; the two ciphertexts of a
 // workgroup stream the same BSK lines, so the second load hits L1.
 //
-// FFT layouts: positions [slot0, slot1, slot2, lane0..lane5] -> index bit.
-//   forward  LA [8,7,6] -swap32,swap16-> LB [5,4] -lds-> LC [3,2,1] -swap32-> LD [0]
-// (swap32 exchanges slot bit 1 with lane bit 5, swap16 slot bit 2 with lane
-// bit 4, so LB holds index bits 8,7 in lane bits 4,5.)
-//   inverse  the exact reverse, ending in LA (natural order: j = lane + 64*slot)
+// FFT: forward LA [8,7,6] -lds-> LB [5,4,3] -lds-> LC [2,1,0]; the inverse
+// is the exact reverse, ending in LA (natural order: j = lane + 64*slot).
 // The accumulator is kept in registers as the top 32 bits of each torus
 // coefficient when L*beta <= 31 (ACC32), else as full u64.
 #pragma once
@@ -31,17 +28,25 @@ constexpr int M = 512, N = 1024, S = 8, K = 2;
 constexpr int G = 2;             // ciphertexts per workgroup
 constexpr int WPC = K + 1;       // waves per ciphertext
 constexpr int NT = 64 * G * WPC; // 384 threads
-constexpr int NTW = 17;          // per-lane twiddle entries (forward stages 8..1)
+constexpr int NTW = 14;          // per-lane twiddle entries (7 per radix-8 pass A, B)
 constexpr int NMAX = 1023;       // max small-LWE dimension (LDS budget: 2 workgroups per CU)
+constexpr int SCR = 528;         // relayout scratch elements per wave (positions < 527)
 
+// Transform = three radix-8 passes over index bits (8,7,6), (5,4,3), (2,1,0).
+// A pass runs a constant DFT-8 network on its 3 slot bits (internal
+// twiddles are 8th roots of unity) and then multiplies element u by the lane
+// twiddle exp(2 pi i L m / 2^(p0+3)), m = bitrev3(u), L = index bits below
+// the pass (the lane-dependent parts of all radix-2 DIF twiddles of the pass,
+// deferred to its end). Pass C has L = 0. Two wave-local LDS relayouts move
+// the slot bits; there are no lane permutes.
+// Layouts: positions [slot0, slot1, slot2, lane0..lane5] -> index bit.
 struct Lay {
   int p[9];
 };
-constexpr Lay LAYS[4] = {{{6, 7, 8, 0, 1, 2, 3, 4, 5}},   // LA
-                         {{6, 5, 4, 0, 1, 2, 3, 8, 7}},   // LB
-                         {{1, 2, 3, 4, 5, 6, 7, 8, 0}},   // LC
-                         {{1, 2, 0, 4, 5, 6, 7, 8, 3}}};  // LD
-enum { LA = 0, LB = 1, LC = 2, LD = 3 };
+constexpr Lay LAYS[3] = {{{6, 7, 8, 0, 1, 2, 3, 4, 5}},   // LA: natural, j = lane + 64 u
+                         {{3, 4, 5, 2, 8, 1, 0, 7, 6}},   // LB
+                         {{0, 1, 2, 5, 6, 7, 3, 4, 8}}};  // LC: transform output
+enum { LA = 0, LB = 1, LC = 2 };
 
 __host__ __device__ constexpr int jof(int li, int lane, int u) {
   int j = 0;
@@ -50,63 +55,33 @@ __host__ __device__ constexpr int jof(int li, int lane, int u) {
   return j;
 }
 
-// LDS position of FFT index j in the relayout scratch: j + j/16 (one pad
-// element per 16). Injective, additive in the lane and slot parts of j (one
-// base register plus immediate offsets) and conflict-free: a ds_read_b128
-// bank quad is the position mod 16 = (j + j/16) mod 16, so the 16-lane read
-// groups (index bits 0..3 and 8 of LB, bits 4..8 of LC) and 8-lane write
-// groups (bits 0..2 of LB, 4..6 of LC) land on distinct quads (bit 8 moves a
-// position by 272 = 0 mod 16).
-constexpr int SCR = M + M / 16;  // scratch elements per wave
-__host__ __device__ constexpr int swz(int j) { return j + (j >> 4); }
+// Scratch position of index j for each relayout: j + sum_k c_k * bit_{4+k}(j)
+// (c superincreasing -> injective; additive in the lane and slot parts, so
+// one base register plus immediate offsets). The offsets were searched so
+// that the 8-lane ds_write_b128 groups of the source layout and the 16-lane
+// ds_read_b128 groups of the target layout hit distinct bank quads.
+enum { R1F = 0, R1I = 1, R2F = 2, R2I = 3 };  // LA->LB, LB->LA, LB->LC, LC->LB
+constexpr int RC[4][5] = {{0, 0, 0, 0, 8}, {0, 0, 0, 0, 1}, {0, 1, 2, 4, 7}, {0, 1, 2, 4, 8}};
+__host__ __device__ constexpr int rpos(int r, int j) {
+  int p = j;
+  for (int k = 0; k < 5; ++k) p += RC[r][k] * ((j >> (4 + k)) & 1);
+  return p;
+}
 
-// Twiddle entries: a DIF stage on slot bit sb of layout li works on index
-// bit k = p[sb]; its twiddle W = exp(2 pi i (j mod 2^k) / 2^(k+1)) depends on
-// the lane and on the slot bits mapped below k ("relevant" bits).
-__host__ __device__ constexpr int stage_k(int li, int sb) { return LAYS[li].p[sb]; }
-__host__ __device__ constexpr int n_rel(int li, int sb) {
-  int c = 0;
-  for (int b = 0; b < 3; ++b)
-    if (b != sb && LAYS[li].p[b] < LAYS[li].p[sb]) ++c;
-  return c;
-}
-// entry offset of pair base u within its stage
-__host__ __device__ constexpr int ent(int li, int sb, int u) {
-  int e = 0, c = 0;
-  for (int b = 0; b < 3; ++b)
-    if (b != sb && LAYS[li].p[b] < LAYS[li].p[sb]) e |= ((u >> b) & 1) << c++;
-  return e;
-}
-// slot value u whose relevant bits encode entry e (inverse of ent)
-__host__ __device__ constexpr int ent_u(int li, int sb, int e) {
-  int u = 0, c = 0;
-  for (int b = 0; b < 3; ++b)
-    if (b != sb && LAYS[li].p[b] < LAYS[li].p[sb]) u |= ((e >> c++) & 1) << b;
-  return u;
-}
-// forward stage list: (layout, slot bit); entry base offsets
-constexpr int NST = 8;
-constexpr int ST_L[NST] = {LA, LA, LA, LB, LB, LC, LC, LC};
-constexpr int ST_B[NST] = {2, 1, 0, 1, 2, 2, 1, 0};
-__host__ __device__ constexpr int st_e0(int s) {
-  int e = 0;
-  for (int t = 0; t < s; ++t) e += 1 << n_rel(ST_L[t], ST_B[t]);
-  return e;
-}
-static_assert(st_e0(NST) == NTW, "twiddle entry count");
+__host__ __device__ constexpr int bitrev3(int u) { return ((u & 1) << 2) | (u & 2) | ((u >> 2) & 1); }
 
-// Fill the per-workgroup LDS tables: twl[e][lane] (stage twiddles) and
-// twt[u][lane] = twist[lane + 64 u] (the fold's w^j, natural layout).
+// Per-lane tables in LDS: twl[e][lane], e = 7 * pass + (m - 1) (passes A, B),
+// and twt[u][lane] = twist[lane + 64 u] (the fold's w^j, natural layout).
 __device__ __forceinline__ void fill_tables(c64* twl, c64* twt, const c64* __restrict__ tw,
                                             const c64* __restrict__ twist, int tid, int nthr) {
   for (int x = tid; x < NTW * 64; x += nthr) {
     const int e = x >> 6, lane = x & 63;
-    int s = 0;
-    while (s + 1 < NST && st_e0(s + 1) <= e) ++s;
-    const int li = ST_L[s], sb = ST_B[s], k = stage_k(li, sb);
-    const int u = ent_u(li, sb, e - st_e0(s));
-    const int jm = jof(li, lane, u) & ((1 << k) - 1);
-    twl[x] = tw[jm * ((M / 2) >> k)];
+    const int pass = e / 7, m = e % 7 + 1;
+    const int p0 = pass == 0 ? 6 : 3;
+    const int L = jof(pass == 0 ? LA : LB, lane, 0) & ((1 << p0) - 1);
+    const int q = (L * m << (6 - p0)) & (M - 1);  // exp(2 pi i q / M)
+    const c64 w = tw[q & (M / 2 - 1)];
+    twl[x] = q < M / 2 ? w : c64{-w.x, -w.y};
   }
   for (int x = tid; x < S * 64; x += nthr) twt[x] = twist[x];
 }
@@ -117,132 +92,117 @@ __device__ __forceinline__ void fill_tables(c64* twl, c64* twt, const c64* __res
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---- register-level pieces ---------------------------------------------
-template <int SB>
-__device__ __forceinline__ void swap32(c64 (&v)[S]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int u = ((q >> SB) << (SB + 1)) | (q & ((1 << SB) - 1)), w = u | (1 << SB);
-    uint64_t xr = __builtin_bit_cast(uint64_t, v[u].x), xi = __builtin_bit_cast(uint64_t, v[u].y);
-    uint64_t yr = __builtin_bit_cast(uint64_t, v[w].x), yi = __builtin_bit_cast(uint64_t, v[w].y);
-    auto a0 = __builtin_amdgcn_permlane32_swap((uint32_t)xr, (uint32_t)yr, false, false);
-    auto a1 = __builtin_amdgcn_permlane32_swap((uint32_t)(xr >> 32), (uint32_t)(yr >> 32), false, false);
-    auto b0 = __builtin_amdgcn_permlane32_swap((uint32_t)xi, (uint32_t)yi, false, false);
-    auto b1 = __builtin_amdgcn_permlane32_swap((uint32_t)(xi >> 32), (uint32_t)(yi >> 32), false, false);
-    v[u].x = __builtin_bit_cast(double, (uint64_t)a0[0] | ((uint64_t)a1[0] << 32));
-    v[w].x = __builtin_bit_cast(double, (uint64_t)a0[1] | ((uint64_t)a1[1] << 32));
-    v[u].y = __builtin_bit_cast(double, (uint64_t)b0[0] | ((uint64_t)b1[0] << 32));
-    v[w].y = __builtin_bit_cast(double, (uint64_t)b0[1] | ((uint64_t)b1[1] << 32));
-  }
-}
-template <int SB>
-__device__ __forceinline__ void swap16(c64 (&v)[S]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int u = ((q >> SB) << (SB + 1)) | (q & ((1 << SB) - 1)), w = u | (1 << SB);
-    uint64_t xr = __builtin_bit_cast(uint64_t, v[u].x), xi = __builtin_bit_cast(uint64_t, v[u].y);
-    uint64_t yr = __builtin_bit_cast(uint64_t, v[w].x), yi = __builtin_bit_cast(uint64_t, v[w].y);
-    auto a0 = __builtin_amdgcn_permlane16_swap((uint32_t)xr, (uint32_t)yr, false, false);
-    auto a1 = __builtin_amdgcn_permlane16_swap((uint32_t)(xr >> 32), (uint32_t)(yr >> 32), false, false);
-    auto b0 = __builtin_amdgcn_permlane16_swap((uint32_t)xi, (uint32_t)yi, false, false);
-    auto b1 = __builtin_amdgcn_permlane16_swap((uint32_t)(xi >> 32), (uint32_t)(yi >> 32), false, false);
-    v[u].x = __builtin_bit_cast(double, (uint64_t)a0[0] | ((uint64_t)a1[0] << 32));
-    v[w].x = __builtin_bit_cast(double, (uint64_t)a0[1] | ((uint64_t)a1[1] << 32));
-    v[u].y = __builtin_bit_cast(double, (uint64_t)b0[0] | ((uint64_t)b1[0] << 32));
-    v[w].y = __builtin_bit_cast(double, (uint64_t)b0[1] | ((uint64_t)b1[1] << 32));
-  }
-}
+constexpr double RH = 0.70710678118654752440;  // sqrt(2)/2
 
-// DIF / DIT stage s of the forward list (twiddles from LDS); stage 0 of the
-// transform (index bit 0, W = 1) is separate.
-// DBG (timing experiments only, results wrong): bit 0 takes every twiddle
-// from the register wf instead of LDS; bit 3 skips the relayout's LDS trip.
-template <int ST, int DBG = 0>
-__device__ __forceinline__ void dif(c64 (&v)[S], const c64* twl, int lane, c64 wf = {}) {
-  constexpr int li = ST_L[ST], SB = ST_B[ST], E0 = st_e0(ST), NE = 1 << n_rel(li, SB);
-  // the stage's distinct twiddles as one batch of LDS reads (one wait)
-  c64 Wt[NE];
+// constant DFT-8 network, DIF (natural -> bit-reversed within the pass)
+__device__ __forceinline__ void dft8(c64 (&v)[S]) {
 #pragma unroll
-  for (int e = 0; e < NE; ++e) Wt[e] = (DBG & 1) ? wf : twl[(E0 + e) * 64 + lane];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int u = ((q >> SB) << (SB + 1)) | (q & ((1 << SB) - 1)), w = u | (1 << SB);
-    const c64 W = Wt[ent(li, SB, u)];
-    const c64 X = v[u], Y = v[w];
+  for (int u = 0; u < 4; ++u) {  // slot bit 2; twiddles 1, w8, i, w8^3
+    const c64 X = v[u], Y = v[u + 4];
     v[u] = cadd(X, Y);
-    v[w] = cmul(csub(X, Y), W);
+    const c64 D = csub(X, Y);
+    if (u == 0) v[4] = D;
+    if (u == 1) v[5] = {(D.x - D.y) * RH, (D.x + D.y) * RH};
+    if (u == 2) v[6] = {-D.y, D.x};
+    if (u == 3) v[7] = {-(D.x + D.y) * RH, (D.x - D.y) * RH};
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // slot bit 1; twiddles 1, i
+    const int u = ((q >> 1) << 2) | (q & 1);
+    const c64 X = v[u], Y = v[u + 2];
+    v[u] = cadd(X, Y);
+    const c64 D = csub(X, Y);
+    v[u + 2] = (u & 1) ? c64{-D.y, D.x} : D;
+  }
+#pragma unroll
+  for (int u = 0; u < S; u += 2) {  // slot bit 0
+    const c64 X = v[u], Y = v[u + 1];
+    v[u] = cadd(X, Y);
+    v[u + 1] = csub(X, Y);
   }
 }
-template <int ST, int DBG = 0>
-__device__ __forceinline__ void dit(c64 (&v)[S], const c64* twl, int lane, c64 wf = {}) {
-  constexpr int li = ST_L[ST], SB = ST_B[ST], E0 = st_e0(ST), NE = 1 << n_rel(li, SB);
-  // the stage's distinct twiddles as one batch of LDS reads (one wait)
-  c64 Wt[NE];
+// its exact inverse up to a factor 8 (DIT, conjugate constants)
+__device__ __forceinline__ void idft8(c64 (&v)[S]) {
 #pragma unroll
-  for (int e = 0; e < NE; ++e) Wt[e] = (DBG & 1) ? wf : twl[(E0 + e) * 64 + lane];
+  for (int u = 0; u < S; u += 2) {
+    const c64 X = v[u], Y = v[u + 1];
+    v[u] = cadd(X, Y);
+    v[u + 1] = csub(X, Y);
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int u = ((q >> SB) << (SB + 1)) | (q & ((1 << SB) - 1)), w = u | (1 << SB);
-    const c64 W = Wt[ent(li, SB, u)];
-    const c64 X = v[u], Y = cmulc(v[w], W);
+    const int u = ((q >> 1) << 2) | (q & 1);
+    const c64 X = v[u], Y0 = v[u + 2];
+    const c64 Y = (u & 1) ? c64{Y0.y, -Y0.x} : Y0;  // * conj(i)
     v[u] = cadd(X, Y);
-    v[w] = csub(X, Y);
+    v[u + 2] = csub(X, Y);
   }
-}
-// index bit 0 on slot bit 2 of LD: W = 1
-__device__ __forceinline__ void bfly0(c64 (&v)[S]) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const c64 X = v[u], Y = v[u + 4];
+    const c64 X = v[u], Y0 = v[u + 4];
+    c64 Y = Y0;
+    if (u == 1) Y = {(Y0.x + Y0.y) * RH, (Y0.y - Y0.x) * RH};    // * exp(-i pi/4)
+    if (u == 2) Y = {Y0.y, -Y0.x};                               // * -i
+    if (u == 3) Y = {(Y0.y - Y0.x) * RH, -(Y0.x + Y0.y) * RH};   // * exp(-3 i pi/4)
     v[u] = cadd(X, Y);
     v[u + 4] = csub(X, Y);
   }
 }
 
-// wave-local relayout through the wave's own scratch (no barrier)
-template <int LS, int LT, int DBG = 0>
+// lane twiddles of pass PS (0 = A, 1 = B); DBG bit 0 takes them from wf
+// (two batches of LDS reads, m = 1..4 then 5..7, to bound register use)
+template <int PS, bool INV, int DBG = 0>
+__device__ __forceinline__ void lane_tw(c64 (&v)[S], const c64* twl, int lane, c64 wf) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int m0 = h ? 5 : 1, m1 = h ? 7 : 4;
+    c64 T[4];
+#pragma unroll
+    for (int m = m0; m <= m1; ++m) T[m - m0] = (DBG & 1) ? wf : twl[(7 * PS + m - 1) * 64 + lane];
+#pragma unroll
+    for (int u = 1; u < S; ++u) {
+      const int m = bitrev3(u);
+      if (m < m0 || m > m1) continue;
+      v[u] = INV ? cmulc(v[u], T[m - m0]) : cmul(v[u], T[m - m0]);
+    }
+  }
+}
+
+// Wave-local relayout through the wave's own scratch: no barrier and no
+// wait between the writes and the reads — one wave's DS operations are
+// performed in order, so its reads see its writes (and a later write cannot
+// overtake an earlier read); the compiler keeps these possibly-aliasing
+// accesses in program order and waits only before the data is used.
+template <int R, int LS, int LT, int DBG = 0>
 __device__ __forceinline__ void relayout(c64 (&v)[S], c64* scr, int lane) {
   if constexpr ((DBG & 8) != 0) return;
 #pragma unroll
-  for (int u = 0; u < S; ++u) scr[swz(jof(LS, lane, u))] = v[u];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int u = 0; u < S; ++u) scr[rpos(R, jof(LS, lane, u))] = v[u];
 #pragma unroll
-  for (int u = 0; u < S; ++u) v[u] = scr[swz(jof(LT, lane, u))];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int u = 0; u < S; ++u) v[u] = scr[rpos(R, jof(LT, lane, u))];
 }
 
-// natural order (LA) -> LD
+// natural order (LA) -> LC
 template <int DBG = 0>
 __device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {}) {
-  dif<0, DBG>(v, twl, lane, wf);
-  dif<1, DBG>(v, twl, lane, wf);
-  dif<2, DBG>(v, twl, lane, wf);
-  swap32<1>(v);
-  swap16<2>(v);
-  dif<3, DBG>(v, twl, lane, wf);
-  dif<4, DBG>(v, twl, lane, wf);
-  relayout<LB, LC, DBG>(v, scr, lane);
-  dif<5, DBG>(v, twl, lane, wf);
-  dif<6, DBG>(v, twl, lane, wf);
-  dif<7, DBG>(v, twl, lane, wf);
-  swap32<2>(v);
-  bfly0(v);
+  dft8(v);
+  lane_tw<0, false, DBG>(v, twl, lane, wf);
+  relayout<R1F, LA, LB, DBG>(v, scr, lane);
+  dft8(v);
+  lane_tw<1, false, DBG>(v, twl, lane, wf);
+  relayout<R2F, LB, LC, DBG>(v, scr, lane);
+  dft8(v);
 }
-// LD -> natural order (LA), times M
+// LC -> natural order (LA), times M
 template <int DBG = 0>
 __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {}) {
-  bfly0(v);
-  swap32<2>(v);
-  dit<7, DBG>(v, twl, lane, wf);
-  dit<6, DBG>(v, twl, lane, wf);
-  dit<5, DBG>(v, twl, lane, wf);
-  relayout<LC, LB, DBG>(v, scr, lane);
-  dit<4, DBG>(v, twl, lane, wf);
-  dit<3, DBG>(v, twl, lane, wf);
-  swap16<2>(v);
-  swap32<1>(v);
-  dit<2, DBG>(v, twl, lane, wf);
-  dit<1, DBG>(v, twl, lane, wf);
-  dit<0, DBG>(v, twl, lane, wf);
+  idft8(v);
+  relayout<R2I, LC, LB, DBG>(v, scr, lane);
+  lane_tw<1, true, DBG>(v, twl, lane, wf);
+  idft8(v);
+  relayout<R1I, LB, LA, DBG>(v, scr, lane);
+  lane_tw<0, true, DBG>(v, twl, lane, wf);
+  idft8(v);
 }
 
 // ---- accumulator word type ------------------------------------------------

@@ -657,7 +657,7 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
 }
 
 // ---- blind rotation v4 (br_v4.h): a wave per GLWE component ---------------
-// BSK conversion: one wave per polynomial, stored [poly][u][lane] (layout LD
+// BSK conversion: one wave per polynomial, stored [poly][u][lane] (layout LC
 // of the forward transform) and scaled by 1/M.
 __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bsk, int npoly,
                                                       const c64* __restrict__ tw, const c64* __restrict__ twist,
@@ -685,31 +685,28 @@ __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bs
   }
 }
 
-// Balanced gadget digits of x (level 0 = most significant) into d[0..L).
+// Balanced gadget digits of x (level 0 = most significant) into d[0..L):
+// round to the top L*beta bits, then LSB-first each digit is the sign
+// extension of its beta bits (>= B/2 becomes negative), subtracted before
+// the next digit is read (that is the carry).
 template <int L, bool A32>
 __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int beta, int (&d)[L]) {
   const int prec = L * beta;
   if constexpr (A32) {
     uint32_t r = ((x >> (31 - prec)) + 1) >> 1;
-    const uint32_t B = 1u << beta, hb = B >> 1;
 #pragma unroll
-    for (int l = L - 1; l >= 0; --l) {
-      const uint32_t dd = r & (B - 1);
-      r >>= beta;
-      const uint32_t cy = dd >= hb;
-      d[l] = (int)dd - (int)(cy << beta);
-      r += cy;
+    for (int i = 0; i < L; ++i) {
+      const int di = __builtin_amdgcn_sbfe((int)r, i * beta, beta);
+      d[L - 1 - i] = di;
+      if (i + 1 < L) r -= (uint32_t)di << (i * beta);
     }
   } else {
     u64 r = ((x >> (63 - prec)) + 1) >> 1;
-    const u64 B = 1ull << beta, hb = B >> 1;
 #pragma unroll
-    for (int l = L - 1; l >= 0; --l) {
-      const u64 dd = r & (B - 1);
-      r >>= beta;
-      const u64 cy = dd >= hb;
-      d[l] = (int)dd - (int)(cy << beta);
-      r += cy;
+    for (int i = 0; i < L; ++i) {
+      const int64_t di = (int64_t)(r << (64 - (i + 1) * beta)) >> (64 - beta);
+      d[L - 1 - i] = (int)di;
+      if (i + 1 < L) r -= (u64)di << (i * beta);
     }
   }
 }
@@ -764,8 +761,7 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
     // X^a ACC - ACC through the wave's slot, then the gadget digits
     if constexpr ((DBG & 16) == 0) {
 #pragma unroll
-      for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];  // own slot: in-order DS, no wait
     }
     c64 v[S];
     uint32_t dg[L > 1 ? L - 1 : 1][S];  // levels >= 1, two int16 digits per word
@@ -775,22 +771,20 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
       const uint32_t src = (uint32_t)(s * 64 + lane - (int)a) & (2 * N - 1);
       rot[s] = (DBG & 16) ? acc[(s + 1) & 15] + (T)src : sa[src & (N - 1)];
     }
+    // coefficient pairs (t, t + N/2) fold into one complex point
 #pragma unroll
-    for (int s = 0; s < 2 * S; ++s) {
-      const uint32_t src = (uint32_t)(s * 64 + lane - (int)a) & (2 * N - 1);
-      T r = rot[s];
-      if (src >= (uint32_t)N) r = (T)0 - r;
-      int d[L];
-      decompose_v4<L, A32>((T)(r - acc[s]), beta, d);
+    for (int s = 0; s < S; ++s) {
+      int d[2][L];
 #pragma unroll
-      for (int l = 1; l < L; ++l) {
-        if (s < S) dg[l - 1][s] = (uint32_t)(d[l] & 0xffff);
-        else dg[l - 1][s - S] |= (uint32_t)d[l] << 16;
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
+        const T r = src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S];
+        decompose_v4<L, A32>((T)(r - acc[s + h * S]), beta, d[h]);
       }
-      if (s < S) v[s].x = (double)d[0];
-      else v[s - S].y = (double)d[0];
+      v[s] = {(double)d[0][0], (double)d[1][0]};
+#pragma unroll
+      for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
     c64 mac[S];
 #pragma unroll
@@ -837,11 +831,14 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
       for (int ci = 0; ci < K; ++ci) {
         const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
         const c64* fs = ctslots + cin * SCR;
-        c64 fv[S];
 #pragma unroll
-        for (int u = 0; u < S; ++u) fv[u] = (DBG & 32) ? v[u] : fs[u * 64 + lane];
+        for (int hh = 0; hh < 2; ++hh) {  // F in halves: bounds register use at the peak
+          c64 fv[S / 2];
 #pragma unroll
-        for (int u = 0; u < S; ++u) cmac(mac[u], fv[u], kx[ci][u]);
+          for (int u = 0; u < S / 2; ++u) fv[u] = (DBG & 32) ? v[hh * 4 + u] : fs[(hh * 4 + u) * 64 + lane];
+#pragma unroll
+          for (int u = 0; u < S / 2; ++u) cmac(mac[hh * 4 + u], fv[u], kx[ci][hh * 4 + u]);
+        }
       }
       if constexpr ((DBG & 4) == 0) lds_barrier();
     }

@@ -23,7 +23,7 @@
 
 namespace fhei {
 
-struct c64 {
+struct alignas(16) c64 {
   double x, y;
 };
 
