@@ -361,6 +361,113 @@ __device__ __forceinline__ void br_emit(int mode, u64 x, bool body, const BrTv& 
   if (sign) sign[pos] = d;
 }
 
+
+// ---- key switch on the i8 matrix cores (v_mfma_i32_16x16x64_i8) ----------
+// out[c] = (0, .., 0, b'[c]) - sum_r D[c][r] * KSK[r], r = i * ks_level + l,
+// a GEMM [count x K] (digits in [-2^(b-1), 2^(b-1))) x [K x (n+1)] over
+// Z_2^64. The key is split into 8 balanced radix-256 byte planes,
+// KSK = sum_q s_q 2^(8q) with s_q in [-128, 127], each an i8 GEMM with i32
+// accumulation (|sum| <= K * 2^(b-1) * 128 < 2^31); the epilogue recombines
+// sum_q acc_q << 8q modulo 2^64 (exact: DESIGN.md §4.3).
+// Fragment layouts (checked by tools/mfma_i8_probe.hip): lane l holds
+// A[row l&15][k = 16 (l>>4) + j] and B[k = 16 (l>>4) + j][col l&15] in byte j;
+// C/D: row 4 (l>>4) + reg, col l&15.
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int KSM_NB_COLS = 16;  // columns per block
+
+// key planes: [kb][nb][q][lane][16 B]
+__global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int n1, int NB, int8_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)K * NB * 16) return;
+  const int row = (int)(e / (NB * 16)), col = (int)(e % (NB * 16));
+  u64 x = col < n1 ? ksk[(size_t)row * n1 + col] : 0;
+  const int kb = row >> 6, g = (row >> 4) & 3, j = row & 15;
+  const int nb = col >> 4, lane = (col & 15) + 16 * g;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int8_t sq = (int8_t)(x & 0xff);
+    x = (x - (u64)(int64_t)sq) >> 8;
+    out[((((size_t)kb * NB + nb) * 8 + q) * 64 + lane) * 16 + j] = sq;
+  }
+}
+
+// digits in A-fragment order [cb][kb][lane][16 B] (ks_level = 4: a
+// coefficient's 4 digits are 4 consecutive bytes) and b' = (b << shift) + add
+__global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, int64_t count, int big, int beta,
+                                                   int shift, u64 add_body, int KB, uint32_t* __restrict__ D,
+                                                   u64* __restrict__ body) {
+  const int t = threadIdx.x, cl = t >> 4, il = t & 15;
+  const int64_t cb = blockIdx.y, c = cb * 16 + cl;
+  const int kb = blockIdx.x, i = kb * 16 + il;
+  if (c >= count) return;
+  const u64* src = in + (size_t)c * (big + 1);
+  if (kb == 0 && il == 0) body[c] = (src[big] << shift) + add_body;
+  const int prec = 4 * beta;
+  uint32_t r = (uint32_t)((((src[i] << shift) >> (63 - prec)) + 1) >> 1);
+  uint32_t packed = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {  // LSB-first; level l = 3 - s sits in byte l
+    const int d = __builtin_amdgcn_sbfe((int)r, s * beta, beta);
+    r -= (uint32_t)d << (s * beta);
+    packed |= (uint32_t)(uint8_t)(int8_t)d << (8 * (3 - s));
+  }
+  const int lane = cl + 16 * (il >> 2);
+  D[(((size_t)cb * KB + kb) * 64 + lane) * 4 + (il & 3)] = packed;
+}
+
+// workgroup = 4 waves = 64 ciphertexts x 16 columns x 8 byte planes; the key
+// tile of each k-block (8 KB) is shared through double-buffered LDS
+__global__ void __launch_bounds__(256) k_keyswitch_mfma(const v4i* __restrict__ D, const v4i* __restrict__ K8,
+                                                        const u64* __restrict__ body, int64_t count, int n1, int NB,
+                                                        int KB, u64* __restrict__ out) {
+  __shared__ v4i bt[2][8 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nb = blockIdx.y;
+  const int64_t cb = (int64_t)blockIdx.x * 4 + w;
+  const bool act = cb * 16 < count;
+  const v4i zero = {0, 0, 0, 0};
+  const v4i* Dv = D + (size_t)cb * KB * 64 + lane;
+  const v4i* Kv = K8 + (size_t)nb * 8 * 64;
+  v4i acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = zero;
+  bt[0][tid] = Kv[tid];
+  bt[0][tid + 256] = Kv[tid + 256];
+  v4i a = act ? Dv[0] : zero;
+  __syncthreads();
+  for (int kb = 0; kb < KB; ++kb) {
+    const int cur = kb & 1;
+    v4i n0 = zero, n1v = zero, an = zero;
+    const bool more = kb + 1 < KB;
+    if (more) {
+      const v4i* srcp = Kv + (size_t)(kb + 1) * NB * 8 * 64;
+      n0 = srcp[tid];
+      n1v = srcp[tid + 256];
+      if (act) an = Dv[(size_t)(kb + 1) * 64];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bt[cur][q * 64 + lane], acc[q], 0, 0, 0);
+    if (more) {
+      bt[cur ^ 1][tid] = n0;
+      bt[cur ^ 1][tid + 256] = n1v;
+      a = an;
+    }
+    __syncthreads();
+  }
+  if (!act) return;
+  const int col = nb * KSM_NB_COLS + (lane & 15);
+  if (col >= n1) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t c = cb * 16 + 4 * (lane >> 4) + r;
+    if (c >= count) continue;
+    u64 v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += (u64)(int64_t)acc[q][r] << (8 * q);
+    out[(size_t)c * n1 + col] = (col == n1 - 1 ? body[c] : (u64)0) - v;
+  }
+}
+
 // Blind rotation + sample extraction. One 64-lane wavefront (= workgroup)
 // per ciphertext; the GLWE accumulator ((K+1) x N u64) lives in LDS, the
 // external-product partial sums in registers.
@@ -963,6 +1070,11 @@ struct fhe_ctx {
   ProfAcc prof_br, prof_ks;
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2, 3
   int v4_dbg = 0;      // timing experiments only (FHEICP_V4_DBG), wrong results
+  // i8-MFMA key switch: key byte planes and a digit/body workspace
+  int8_t* ksk8 = nullptr;
+  void* ks_ws = nullptr;
+  size_t ks_ws_bytes = 0;
+  int ks_variant = 2;  // 2 = MFMA (default when ks_level == 4), 1 = VALU split-K
 };
 
 static std::mutex g_err_mu;
@@ -1040,6 +1152,8 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
     ctx->br_variant = (v == 2 || v == 3 || v == 4) ? v : 4;
   }
   if (const char* e = getenv("FHEICP_V4_DBG")) ctx->v4_dbg = atoi(e);
+  if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
+  if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
   if (ctx->br_variant == 4 && !(params->k == 2 && params->n <= v4::NMAX && params->pbs_level <= 7 &&
                                  (params->pbs_level == 1 || params->pbs_base_log <= 16)))
@@ -1090,6 +1204,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     hipSetDevice(ctx->device);
     hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk); hipFree(ctx->ksk_colsum);
     hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
+    hipFree(ctx->ksk8); hipFree(ctx->ks_ws);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_ks);
   }
@@ -1135,6 +1250,13 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
   const fhe_params& p = ctx->p;
   hipLaunchKernelGGL(k_ksk_colsum, dim3((p.n + 1 + 255) / 256), dim3(256), 0, st, ctx->ksk, p.k * p.N * p.ks_level,
                      p.n, ctx->ksk_colsum);
+  if (ctx->ks_variant == 2) {
+    const int K = p.k * p.N * p.ks_level, n1 = p.n + 1, NB = (n1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
+    if (!ctx->ksk8) HIPCHK(ctx, hipMalloc(&ctx->ksk8, (size_t)K * NB * 16 * 8));
+    const int64_t tot = (int64_t)K * NB * 16;
+    hipLaunchKernelGGL(k_ksk_to_i8, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ctx->ksk, K, n1, NB,
+                       ctx->ksk8);
+  }
   const int npoly = (int)(fhe_bsk_words(&p) / p.N);
   switch (p.N) {
     case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
@@ -1294,6 +1416,32 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   hipStream_t st = (hipStream_t)stream;
   const int64_t tiles = (count + KS_TC - 1) / KS_TC;
   if (tiles > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
+  if (ctx->ks_variant == 2) {
+    const int K = p.k * p.N * p.ks_level, KB = K / 64, n1 = p.n + 1, NB = (n1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
+    const int64_t ncb = (count + 15) / 16;
+    const size_t dbytes = (size_t)ncb * 16 * K, need = dbytes + 8 * (size_t)count;
+    if (need > ctx->ks_ws_bytes) {
+      if (ctx->ks_ws) {
+        HIPCHK(ctx, hipDeviceSynchronize());
+        HIPCHK(ctx, hipFree(ctx->ks_ws));
+        ctx->ks_ws = nullptr;
+      }
+      HIPCHK(ctx, hipMalloc(&ctx->ks_ws, need));
+      ctx->ks_ws_bytes = need;
+    }
+    if (ncb > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
+    uint32_t* D = (uint32_t*)ctx->ks_ws;
+    u64* body = (u64*)((char*)ctx->ks_ws + dbytes);
+    hipEvent_t e1;
+    prof_begin(ctx, ctx->prof_ks, st, &e1);
+    hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)KB, (unsigned)ncb), dim3(256), 0, st, d_big, count, p.k * p.N,
+                       p.ks_base_log, shift, add_body, KB, D, body);
+    hipLaunchKernelGGL(k_keyswitch_mfma, dim3((unsigned)((count + 63) / 64), (unsigned)NB), dim3(256), 0, st,
+                       (const v4i*)D, (const v4i*)ctx->ksk8, body, count, n1, NB, KB, d_small);
+    prof_end(ctx, ctx->prof_ks, st, e1, count);
+    HIPCHK(ctx, hipGetLastError());
+    return FHE_OK;
+  }
   HIPCHK(ctx, hipMemsetAsync(d_small, 0, 8 * (size_t)count * (p.n + 1), st));
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_ks, st, &e1);
