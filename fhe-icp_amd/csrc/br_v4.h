@@ -28,7 +28,7 @@ constexpr int M = 512, N = 1024, S = 8, K = 2;
 constexpr int G = 2;             // ciphertexts per workgroup
 constexpr int WPC = K + 1;       // waves per ciphertext
 constexpr int NT = 64 * G * WPC; // 384 threads
-constexpr int NTW = 14;          // per-lane twiddle entries (7 per radix-8 pass A, B)
+constexpr int NTW = 15;          // per-lane twiddle entries: 8 for pass A (twist merged), 7 for pass B
 constexpr int NMAX = 1023;       // max small-LWE dimension (LDS budget: 2 workgroups per CU)
 constexpr int SCR = 528;         // relayout scratch elements per wave (positions < 527)
 
@@ -70,20 +70,17 @@ __host__ __device__ constexpr int rpos(int r, int j) {
 
 __host__ __device__ constexpr int bitrev3(int u) { return ((u & 1) << 2) | (u & 2) | ((u >> 2) & 1); }
 
-// Per-lane tables in LDS: twl[e][lane], e = 7 * pass + (m - 1) (passes A, B),
-// and twt[u][lane] = twist[lane + 64 u] (the fold's w^j, natural layout).
-__device__ __forceinline__ void fill_tables(c64* twl, c64* twt, const c64* __restrict__ tw,
-                                            const c64* __restrict__ twist, int tid, int nthr) {
-  for (int x = tid; x < NTW * 64; x += nthr) {
-    const int e = x >> 6, lane = x & 63;
-    const int pass = e / 7, m = e % 7 + 1;
-    const int p0 = pass == 0 ? 6 : 3;
-    const int L = jof(pass == 0 ? LA : LB, lane, 0) & ((1 << p0) - 1);
-    const int q = (L * m << (6 - p0)) & (M - 1);  // exp(2 pi i q / M)
-    const c64 w = tw[q & (M / 2 - 1)];
-    twl[x] = q < M / 2 ? w : c64{-w.x, -w.y};
-  }
-  for (int x = tid; x < S * 64; x += nthr) twt[x] = twist[x];
+// Per-lane twiddles, twl[e][lane], computed on the host in long double
+// (v4_twiddles) and copied to LDS per workgroup:
+//   e = m (0..7):      pass A, w^lane * exp(2 pi i lane m / 512) — the lane
+//                      part w^lane of the fold twist w^(lane + 64 u)
+//                      (w = exp(i pi / N)) commutes with pass A's DFT-8 and
+//                      merges into its lane twiddles;
+//   e = 7 + m (1..7):  pass B, exp(2 pi i L m / 64), L = index bits 0..2.
+// The slot part w^(64 u) = exp(i pi u / 16) is a compile-time constant (fold8).
+__host__ __device__ inline int v4_tw_pass(int e) { return e < 8 ? 0 : 1; }
+__device__ __forceinline__ void fill_tables(c64* twl, const c64* __restrict__ tw4, int tid, int nthr) {
+  for (int x = tid; x < NTW * 64; x += nthr) twl[x] = tw4[x];
 }
 
 // Workgroup barrier for LDS hand-offs only: retire this wave's LDS ops, then
@@ -149,22 +146,37 @@ __device__ __forceinline__ void idft8(c64 (&v)[S]) {
   }
 }
 
-// lane twiddles of pass PS (0 = A, 1 = B); DBG bit 0 takes them from wf
-// (two batches of LDS reads, m = 1..4 then 5..7, to bound register use)
+// lane twiddles of pass PS (0 = A: elements 0..7, entries m; 1 = B: elements
+// 1..7, entries 7 + m), in two batches of LDS reads to bound register use;
+// DBG bit 0 takes them from wf
 template <int PS, bool INV, int DBG = 0>
 __device__ __forceinline__ void lane_tw(c64 (&v)[S], const c64* twl, int lane, c64 wf) {
+  constexpr int M0 = PS == 0 ? 0 : 1, E0 = PS == 0 ? 0 : 7;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int m0 = h ? 5 : 1, m1 = h ? 7 : 4;
+    const int m0 = h ? 4 : M0, m1 = h ? 7 : 3;
     c64 T[4];
 #pragma unroll
-    for (int m = m0; m <= m1; ++m) T[m - m0] = (DBG & 1) ? wf : twl[(7 * PS + m - 1) * 64 + lane];
+    for (int m = m0; m <= m1; ++m) T[m - m0] = (DBG & 1) ? wf : twl[(E0 + m) * 64 + lane];
 #pragma unroll
-    for (int u = 1; u < S; ++u) {
+    for (int u = 0; u < S; ++u) {
       const int m = bitrev3(u);
       if (m < m0 || m > m1) continue;
       v[u] = INV ? cmulc(v[u], T[m - m0]) : cmul(v[u], T[m - m0]);
     }
+  }
+}
+
+// the slot part of the fold twist, exp(i pi u / 16) (conjugate when INV)
+template <bool INV>
+__device__ __forceinline__ void fold8(c64 (&v)[S]) {
+  constexpr double C[8] = {1.0, 0.98078528040323044913, 0.92387953251128675613, 0.83146961230254523708,
+                           0.70710678118654752440, 0.55557023301960222474, 0.38268343236508977173,
+                           0.19509032201612826785};
+#pragma unroll
+  for (int u = 1; u < S; ++u) {
+    const c64 c = {C[u], INV ? -C[8 - u] : C[8 - u]};  // sin(pi u/16) = cos(pi (8-u)/16)
+    v[u] = cmul(v[u], c);
   }
 }
 
@@ -182,9 +194,11 @@ __device__ __forceinline__ void relayout(c64 (&v)[S], c64* scr, int lane) {
   for (int u = 0; u < S; ++u) v[u] = scr[rpos(R, jof(LT, lane, u))];
 }
 
-// natural order (LA) -> LC
+// folded coefficient pairs (a_t + i a_{t+M}), natural order (LA) -> LC;
+// includes the negacyclic twist w^t
 template <int DBG = 0>
 __device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {}) {
+  fold8<false>(v);
   dft8(v);
   lane_tw<0, false, DBG>(v, twl, lane, wf);
   relayout<R1F, LA, LB, DBG>(v, scr, lane);
@@ -193,7 +207,7 @@ __device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, i
   relayout<R2F, LB, LC, DBG>(v, scr, lane);
   dft8(v);
 }
-// LC -> natural order (LA), times M
+// LC -> natural order (LA), times M, untwisted
 template <int DBG = 0>
 __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {}) {
   idft8(v);
@@ -203,6 +217,7 @@ __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, i
   relayout<R1I, LB, LA, DBG>(v, scr, lane);
   lane_tw<0, true, DBG>(v, twl, lane, wf);
   idft8(v);
+  fold8<true>(v);
 }
 
 // ---- accumulator word type ------------------------------------------------

@@ -767,14 +767,12 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
 // BSK conversion: one wave per polynomial, stored [poly][u][lane] (layout LC
 // of the forward transform) and scaled by 1/M.
 __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bsk, int npoly,
-                                                      const c64* __restrict__ tw, const c64* __restrict__ twist,
-                                                      c64* __restrict__ out) {
+                                                      const c64* __restrict__ tw4, c64* __restrict__ out) {
   using namespace v4;
   __shared__ c64 twl[NTW * 64];
-  __shared__ c64 twt[S * 64];
   __shared__ c64 scr[SCR];
   const int lane = threadIdx.x;
-  fill_tables(twl, twt, tw, twist, lane, 64);
+  fill_tables(twl, tw4, lane, 64);
   __syncthreads();
   const double inv = 1.0 / (double)M;
   for (int poly = blockIdx.x; poly < npoly; poly += gridDim.x) {
@@ -783,7 +781,7 @@ __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bs
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int t = u * 64 + lane;
-      v[u] = cmul({(double)(int64_t)src[t], (double)(int64_t)src[t + M]}, twt[t]);
+      v[u] = {(double)(int64_t)src[t], (double)(int64_t)src[t + M]};
     }
     forward(v, twl, scr, lane);
     c64* dst = out + (size_t)poly * M;
@@ -824,8 +822,7 @@ __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int bet
 template <int L, bool A32, int DBG = 0>
 __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
-                                                              const c64* __restrict__ tw,
-                                                              const c64* __restrict__ twist, BrTv tv, int mode,
+                                                              const c64* __restrict__ tw4, BrTv tv, int mode,
                                                               u64* __restrict__ out, u64* __restrict__ ct_v,
                                                               u64* __restrict__ refreshed, u64* __restrict__ sign) {
   using namespace v4;
@@ -833,7 +830,6 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
   using T = typename AT::T;
   __shared__ c64 xbuf[G * WPC * SCR];  // one 8.5 KB slot per wave
   __shared__ c64 twl[NTW * 64];
-  __shared__ c64 twt[S * 64];
   __shared__ uint16_t atab[G][NMAX + 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -843,7 +839,7 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
   const c64* ctslots = xbuf + g * WPC * SCR;
   T* sa = reinterpret_cast<T*>(slot);
 
-  fill_tables(twl, twt, tw, twist, tid, NT);
+  fill_tables(twl, tw4, tid, NT);
   for (int x = tid; x < G * (n + 1); x += NT) {
     const int gg = x / (n + 1), ii = x - gg * (n + 1);
     const int64_t cc = (int64_t)blockIdx.x * G + gg;
@@ -904,14 +900,7 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
         for (int u = 0; u < S; ++u)
           v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
       }
-      {
-        c64 tws[S];
-#pragma unroll
-        for (int u = 0; u < S; ++u) tws[u] = twt[u * 64 + lane];
-#pragma unroll
-        for (int u = 0; u < S; ++u) v[u] = cmul(v[u], tws[u]);
-      }
-      // own-component BSK row: loads fly during the transform
+      // own-component BSK row: loads fly during the transform (which folds the twist in)
       c64 kb[S];
       {
         const c64* gp = Gi + ((size_t)(comp * L + lv) * WPC + comp) * M;
@@ -950,14 +939,10 @@ __global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __rest
       if constexpr ((DBG & 4) == 0) lds_barrier();
     }
     inverse<DBG>(mac, twl, slot, lane, wf);
-    c64 tws[S];
-#pragma unroll
-    for (int u = 0; u < S; ++u) tws[u] = twt[u * 64 + lane];
 #pragma unroll
     for (int u = 0; u < S; ++u) {
-      const c64 z = cmulc(mac[u], tws[u]);
-      acc[u] += AT::from_f64(z.x);
-      acc[u + S] += AT::from_f64(z.y);
+      acc[u] += AT::from_f64(mac[u].x);
+      acc[u + S] += AT::from_f64(mac[u].y);
     }
   }
 
@@ -1062,7 +1047,7 @@ struct fhe_ctx {
   std::string err;
   bool keys = false;
   u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
-  c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr;
+  c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr, *tw4 = nullptr;
   // workspace
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -1178,6 +1163,26 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
       const long double ang = 3.14159265358979323846264338327950288L * (long double)t / (long double)N;
       twist[t] = {(double)cosl(ang), (double)sinl(ang)};
     }
+    if (N == 1024) {  // v4 per-lane twiddles (br_v4.h), long double
+      const long double PI = 3.14159265358979323846264338327950288L;
+      std::vector<c64> t4(v4::NTW * 64);
+      for (int e = 0; e < v4::NTW; ++e)
+        for (int lane = 0; lane < 64; ++lane) {
+          long double ang;
+          if (e < 8) {
+            ang = PI * (long double)lane * (long double)(1 + 4 * e) / 1024.0L;
+          } else {
+            const int m = e - 7, L = v4::jof(v4::LB, lane, 0) & 7;
+            ang = 2.0L * PI * (long double)(L * m) / 64.0L;
+          }
+          t4[e * 64 + lane] = {(double)cosl(ang), (double)sinl(ang)};
+        }
+      if (hipMalloc(&ctx->tw4, sizeof(c64) * t4.size()) != hipSuccess ||
+          hipMemcpy(ctx->tw4, t4.data(), sizeof(c64) * t4.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        fhe_ctx_destroy(ctx);
+        return fail(nullptr, FHE_E_DEVICE, "twiddle upload failed");
+      }
+    }
     if (hipMalloc(&ctx->tw, sizeof(c64) * tw.size()) != hipSuccess ||
         hipMalloc(&ctx->twist, sizeof(c64) * twist.size()) != hipSuccess ||
         hipMemcpy(ctx->tw, tw.data(), sizeof(c64) * tw.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1204,7 +1209,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     hipSetDevice(ctx->device);
     hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk); hipFree(ctx->ksk_colsum);
     hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
-    hipFree(ctx->ksk8); hipFree(ctx->ks_ws);
+    hipFree(ctx->ksk8); hipFree(ctx->ks_ws); hipFree(ctx->tw4);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_ks);
   }
@@ -1263,8 +1268,8 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
     case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
     case 1024:
       if (ctx->br_variant == 4)
-        hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw,
-                           ctx->twist, ctx->bsk_fft);
+        hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw4,
+                           ctx->bsk_fft);
       else if (ctx->br_variant == 3)
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
       else
@@ -1468,11 +1473,11 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
 #define BR2(K) do { if (ctx->br_variant == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
 #define BR4(L, A32)                                                                                           \
   hipLaunchKernelGGL((k_blind_rotate_v4<L, A32>), dim3((unsigned)((count + v4::G - 1) / v4::G)), dim3(v4::NT), 0, \
-                     st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, \
+                     st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, mode, out, ct_v,          \
                      refreshed, sign)
 #define BR4D(D)                                                                                               \
   hipLaunchKernelGGL((k_blind_rotate_v4<2, true, D>), dim3((unsigned)((count + v4::G - 1) / v4::G)), dim3(v4::NT), \
-                     0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out,     \
+                     0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, mode, out,               \
                      ct_v, refreshed, sign)
   if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
       p.pbs_level * p.pbs_base_log <= 31) {
