@@ -820,7 +820,7 @@ __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int bet
 // 1 twiddles from a register, 2 no BSK loads, 4 no barriers, 8 no FFT
 // relayout, 16 no LDS rotation, 32 no LDS reads of the other components.
 template <int L, bool A32, int DBG = 0>
-__global__ void __launch_bounds__(v4::NT, 3) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
+__global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
                                                               const c64* __restrict__ tw4, BrTv tv, int mode,
                                                               u64* __restrict__ out, u64* __restrict__ ct_v,
@@ -1140,7 +1140,9 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
   if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
-  if (ctx->br_variant == 4 && !(params->k == 2 && params->n <= v4::NMAX && params->pbs_level <= 7 &&
+  // (measured: v4 wins at gadget levels <= 3, e.g. 21.6 vs 23.6 ms at P=21; from
+  // level 4 its 64-bit accumulator spills and v2 is faster, 40.6 vs 53.0 ms at P=26)
+  if (ctx->br_variant == 4 && !(params->k == 2 && params->n <= v4::NMAX && params->pbs_level <= 3 &&
                                  (params->pbs_level == 1 || params->pbs_base_log <= 16)))
     ctx->br_variant = 2;
   if (device >= 0) {
@@ -1497,11 +1499,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       case 1: if (a32) BR4(1, true); else BR4(1, false); break;
       case 2: if (a32) BR4(2, true); else BR4(2, false); break;
       case 3: BR4(3, false); break;
-      case 4: BR4(4, false); break;
-      case 5: BR4(5, false); break;
-      case 6: BR4(6, false); break;
-      case 7: BR4(7, false); break;
-      default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: pbs_level > 7");
+      default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: pbs_level > 3");
     }
   } else if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
