@@ -79,6 +79,14 @@ def shard(args, rank):
     return q, docs
 
 
+def config_tag(args) -> str:
+    """Which BASELINE.json config this run is (configs[1] is the metric's)."""
+    known = {(1024, 16, 6): "configs[1]", (10000, 32, 8): "configs[2] (one GPU)",
+             (12500, 16, 6): "configs[3], one GPU's share of 100k docs", (1000, 768, 8): "configs[4]"}
+    tag = known.get((args.docs, args.dim, args.n_bits))
+    return f" (BASELINE {tag})" if tag else " (custom)"
+
+
 def br_flops_per_ct(p) -> float:
     """Analytic f64 FLOPs of one blind rotation."""
     M = p.N // 2
@@ -180,8 +188,8 @@ def main():
         "dtype": "u64",
         "data": "synthetic",
         "config": {
-            "workload": f"batch compare 1 query x {B} encrypted docs per GPU, {args.dim}-dim, n_bits={args.n_bits} "
-                        f"(BASELINE configs[1]) + encrypted threshold (min_similarity {args.min_similarity}) "
+            "workload": f"batch compare 1 query x {B} encrypted docs per GPU, {args.dim}-dim, n_bits={args.n_bits}"
+                        f"{config_tag(args)} + encrypted threshold (min_similarity {args.min_similarity}) "
                         f"+ top-{args.top_k}" + (" + RCCL top-k all-gather" if world > 1 else ""),
             "docs_per_gpu": B, "dim": args.dim, "n_bits": args.n_bits, "msg_bits_P": P,
             "pbs_per_compare": n_pbs, "keyswitch_per_compare": n_pbs,
