@@ -60,8 +60,14 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one process per GPU; FHEICP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+        backend = os.environ.get("FHEICP_DIST_BACKEND", "nccl")
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     return world, rank, local
 
 
@@ -148,7 +154,8 @@ def main():
     ks = eng.profile_read("keyswitch")
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        on_dev = torch.distributed.get_backend() == "nccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if on_dev else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -216,6 +223,8 @@ def main():
         "keyswitch_ms_total": round(ks["total_ms"], 3),
     }
 
+    if rank == 0:
+        out["topk_check"] = topk_check(args, model, world, oa, oi)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["parity"] = cpu_leg(args, model, q_np, docs_np, acc, below, T)
 
@@ -223,6 +232,26 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def topk_check(args, model, world, oa, oi):
+    """The merged encrypted top-k of the last step (identical on every rank)
+    against the global top-k of the product's clear quantized path over all
+    ranks' shards: batch_operations.py:278-284 semantics (score >= t, stable
+    sort by score desc, global document index breaking ties)."""
+    scores = []
+    for r in range(world):
+        q, docs = shard(args, r)
+        scores.append(model.predict_clear(q[None, :] * docs))
+    sc = np.concatenate(scores)
+    keep = [(i, float(sc[i])) for i in range(len(sc)) if sc[i] >= args.min_similarity]
+    keep.sort(key=lambda x: x[1], reverse=True)
+    ref_idx = [i for i, _ in keep[:args.top_k]]
+    got = [int(i) for i in oi.cpu().tolist() if i >= 0]
+    s = np.float64(model.qparams.out_scale)
+    got_scores = [float(s * np.float64(a)) for a, i in zip(oa.cpu().tolist(), oi.cpu().tolist()) if i >= 0]
+    return {"docs": int(len(sc)), "k": args.top_k, "indices_equal": got == ref_idx,
+            "scores_equal": got_scores == [sc_ for _, sc_ in keep[:args.top_k]]}
 
 
 def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):

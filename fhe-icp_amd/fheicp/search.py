@@ -23,11 +23,16 @@ def sharded_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx
     oa, oi = topk_fn(acc, below, k, base_idx)
     if world == 1:
         return oa, oi
-    ga = [torch.empty_like(oa) for _ in range(world)]
-    gi = [torch.empty_like(oi) for _ in range(world)]
-    torch.distributed.all_gather(ga, oa, group=group)
-    torch.distributed.all_gather(gi, oi, group=group)
-    cat_a, cat_i = torch.cat(ga), torch.cat(gi)
+    # RCCL gathers device tensors in place; other backends (gloo rehearsals)
+    # go through host copies
+    dev = oa.device
+    host = dev.type != "cpu" and torch.distributed.get_backend(group) != "nccl"
+    sa, si = (oa.cpu(), oi.cpu()) if host else (oa, oi)
+    ga = [torch.empty_like(sa) for _ in range(world)]
+    gi = [torch.empty_like(si) for _ in range(world)]
+    torch.distributed.all_gather(ga, sa, group=group)
+    torch.distributed.all_gather(gi, si, group=group)
+    cat_a, cat_i = torch.cat(ga).to(dev), torch.cat(gi).to(dev)
     ma, pos = topk_fn(cat_a, (cat_i < 0).to(torch.int64), k, 0)
     mi = torch.where(pos >= 0, cat_i[pos.clamp(min=0)], pos)
     return ma, mi
