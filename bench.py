@@ -117,7 +117,7 @@ def main():
     p = eng.params
     P = model.msg_bits
     from fheicp.params import sign_pbs_count
-    n_pbs = sign_pbs_count(P)
+    n_pbs = sign_pbs_count(p)
     from fheicp.model import threshold_int
     from fheicp.search import sharded_topk
     T = threshold_int(model.qparams, args.min_similarity)
@@ -287,7 +287,7 @@ def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
     t_total = time.perf_counter() - t0
     parity["cpu_oracle_acc_matches"] = bool(np.array_equal(v + T, acc_ref[:C]))
     parity["cpu_oracle_threshold_matches"] = bool(np.array_equal(bits, (acc_ref[:C] < T).astype(np.int64)))
-    n_pbs = R.sign_pbs_count(model.msg_bits)
+    n_pbs = R.sign_pbs_count(p)
     base = {
         "value": round(C / t_total, 4),
         "unit": "compares/s",

@@ -816,9 +816,18 @@ __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int bet
   }
 }
 
+// Phase timestamps (DBG bit 7): wave 0 of workgroup 0 records s_memtime at
+// the phase boundaries of steps 100..103 (tools/prof_br.py --stamps).
+__device__ unsigned long long g_v4_stamps[4][16];
+#define V4_STAMP(k)                                                                        \
+  do {                                                                                     \
+    if constexpr ((DBG & 128) != 0) stamp_[k] = __builtin_amdgcn_s_memtime();              \
+  } while (0)
+
 // DBG != 0 only for timing experiments (tools/prof_br.py, FHEICP_V4_DBG):
 // 1 twiddles from a register, 2 no BSK loads, 4 no barriers, 8 no FFT
-// relayout, 16 no LDS rotation, 32 no LDS reads of the other components.
+// relayout, 16 no LDS rotation, 32 no LDS reads of the other components,
+// 128 phase timestamps (results correct).
 template <int L, bool A32, int DBG = 0>
 __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
@@ -861,6 +870,8 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
   const c64 wf = {0.5 + (double)beta * 1e-3, (double)L * 1e-3};  // DBG stand-in value
   for (int i = 0; i < n; ++i) {
     const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)atab[g][i]);
+    [[maybe_unused]] unsigned long long stamp_[14];
+    V4_STAMP(0);
     // X^a ACC - ACC through the wave's slot, then the gadget digits
     if constexpr ((DBG & 16) == 0) {
 #pragma unroll
@@ -889,6 +900,7 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
       for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
     }
 
+    V4_STAMP(1);
     c64 mac[S];
 #pragma unroll
     for (int u = 0; u < S; ++u) mac[u] = {0.0, 0.0};
@@ -908,6 +920,7 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
         for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gp[u * 64 + lane];
       }
       forward<DBG>(v, twl, slot, lane, wf);
+      V4_STAMP(2 + 5 * lv);
 #pragma unroll
       for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
       // own component first (no other wave needed), then the two other rows'
@@ -922,7 +935,9 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
 #pragma unroll
         for (int u = 0; u < S; ++u) kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
       }
+      V4_STAMP(3 + 5 * lv);
       if constexpr ((DBG & 4) == 0) lds_barrier();
+      V4_STAMP(4 + 5 * lv);
 #pragma unroll
       for (int ci = 0; ci < K; ++ci) {
         const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
@@ -936,14 +951,25 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
           for (int u = 0; u < S / 2; ++u) cmac(mac[hh * 4 + u], fv[u], kx[ci][hh * 4 + u]);
         }
       }
+      V4_STAMP(5 + 5 * lv);
       if constexpr ((DBG & 4) == 0) lds_barrier();
+      V4_STAMP(6 + 5 * lv);
     }
     inverse<DBG>(mac, twl, slot, lane, wf);
+    V4_STAMP(12);
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       acc[u] += AT::from_f64(mac[u].x);
       acc[u + S] += AT::from_f64(mac[u].y);
     }
+    V4_STAMP(13);
+    if constexpr ((DBG & 128) != 0)
+      if (blockIdx.x == 0 && w == 0 && i >= 100 && i < 104 && lane < 14) {
+        unsigned long long t_ = 0;
+#pragma unroll
+        for (int k = 0; k < 14; ++k) t_ = lane == k ? stamp_[k] : t_;
+        g_v4_stamps[i - 100][lane] = t_;
+      }
   }
 
   // sample extraction of coefficient 0: mask word t of component comp < K
@@ -1100,7 +1126,39 @@ static int validate(const fhe_params* p, std::string& why) {
   if (p->lwe_noise_bits < 0 || p->lwe_noise_bits > 60 || p->glwe_noise_bits < 0 || p->glwe_noise_bits > 60) {
     why = "noise bits out of range"; return -1;
   }
+  if (p->sign_digit_bits != 0 && (p->sign_digit_bits < 3 || p->sign_digit_bits > 4)) {
+    why = "sign_digit_bits must be 0 (auto), 3 or 4"; return -1;
+  }
   return 0;
+}
+
+static double tuniform_var(int b) { return (std::ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
+
+// Decision margin in sigmas of the worst round of a d-bit digit sign
+// extraction: the staircase round of the lowest digit, margin 2^-(d+1) of the
+// torus, the preceding bootstrap's noise amplified by 2^(P-d), plus key
+// switch and modulus switch noise. Same model as fheicp/params.py
+// noise_report.
+static double digit_margin_sigmas(const fhe_params& p, int d) {
+  const double q2 = std::ldexp(1.0, 128);
+  const double s2_bsk = tuniform_var(p.glwe_noise_bits) / q2, s2_ksk = tuniform_var(p.lwe_noise_bits) / q2;
+  const double B = std::ldexp(1.0, p.pbs_base_log), Bk = std::ldexp(1.0, p.ks_base_log);
+  const double rows = (double)p.pbs_level * (p.k + 1) * p.N;
+  const double v_pbs = p.n * rows * (B * B + 2) / 12.0 * s2_bsk +
+                       p.n * (1 + p.k * p.N / 2.0) / (12.0 * std::pow(B, 2.0 * p.pbs_level));
+  const double v_ks = (double)p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk +
+                      p.k * p.N / 2.0 * std::ldexp(1.0, -2 * p.ks_level * p.ks_base_log) / 12.0;
+  const double v_ms = (p.n / 2.0 + 1) / 12.0 / ((2.0 * p.N) * (2.0 * p.N));
+  const double v = v_pbs * std::ldexp(1.0, 2 * (p.msg_bits - d)) + v_ks + v_ms;
+  return std::ldexp(1.0, -(d + 1)) / std::sqrt(v);
+}
+
+static int sign_digits(const fhe_params& p) {
+  if (p.msg_bits < 4) return 0;
+  if (p.sign_digit_bits) return std::min(p.sign_digit_bits, (int)p.msg_bits);
+  for (int d = std::min(4, (int)p.msg_bits); d > 3; --d)
+    if (digit_margin_sigmas(p, d) >= 9.2) return d;
+  return 3;
 }
 
 extern "C" {
@@ -1491,6 +1549,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       case 16: BR4D(16); break;
       case 32: BR4D(32); break;
       case 6: BR4D(6); break;
+      case 128: BR4D(128); break;
       default: BR4D(63); break;
     }
   } else if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4) {
@@ -1574,16 +1633,25 @@ static int bit_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* 
   return FHE_OK;
 }
 
-// Sign of the msg_bits-bit value v in d_ct_v (consumed) with 3-bit digits
-// (DESIGN.md §3.4): the low m = P - 3 bits are cleared LSB-first, each full
-// digit [b, b+3) by two bootstraps (its top bit by a sign bootstrap; then,
-// with a zero padding bit, its two low bits by a 4-slot staircase LUT),
-// leftover bits by single-bit rounds; the top digit's MSB is the sign.
-int fhe_sign_pbs_count(int32_t msg_bits) {
-  if (msg_bits < 1) return 0;
-  if (msg_bits < 4) return msg_bits;
-  const int m = msg_bits - 3;
-  return 2 * (m / 3) + m % 3 + 1;
+// Sign of the msg_bits-bit value v in d_ct_v (consumed) with d-bit digits
+// (DESIGN.md §3.4): the low m = P - d bits are cleared LSB-first, each full
+// digit [b, b+c) by two bootstraps (its top bit by a sign bootstrap; then,
+// with a zero padding bit, its c-1 low bits by a 2^(c-1)-slot staircase LUT),
+// a leftover of 1-2 bits by single-bit rounds; the sign of the top d bits is
+// the sign of v.
+int fhe_sign_digit_bits(const fhe_params* params) {
+  std::string why;
+  if (validate(params, why)) return -1;
+  return sign_digits(*params);
+}
+
+int fhe_sign_pbs_count(const fhe_params* params) {
+  std::string why;
+  if (validate(params, why)) return -1;
+  const int P = params->msg_bits, d = sign_digits(*params);
+  if (P < 4) return P;
+  const int m = P - d, r = m % d;
+  return 2 * (m / d) + (r >= 3 ? 2 : r) + 1;
 }
 
 static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
@@ -1600,19 +1668,26 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
     }
     return FHE_OK;
   }
-  const int m = P - 3;
+  const int d = sign_digits(p), m = P - d;
+  // one c-bit digit at bit b: the pair of rounds on v << (P-b-c) centred by 2^(63-c)
+  auto digit = [&](int b, int c) -> int {
+    int r;
+    // digit MSB (bit b+c-1): sign bootstrap, ct_v -= [bit] * 2^(b+c-1) * Delta
+    if ((r = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - c, 1ull << (63 - c), small, st))) return r;
+    if ((r = launch_br(ctx, small, count, BrTv{1ull << (62 - P + b + c), 0, 0}, 1, nullptr, d_ct_v, nullptr,
+                       nullptr, st)))
+      return r;
+    // bits [b, b+c-1): top bit is now 0 -> 2^(c-1)-slot staircase, output D' * 2^b * Delta
+    if ((r = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - c, 1ull << (63 - c), small, st))) return r;
+    return launch_br(ctx, small, count, BrTv{0, 1ull << (64 - P + b), logN - (c - 1)}, 2, nullptr, d_ct_v,
+                     nullptr, nullptr, st);
+  };
   int b = 0;
-  for (; b + 3 <= m; b += 3) {
-    // digit MSB (bit b+2): sign bootstrap of v << (P-b-3) centred by 2^60
-    if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 3, 1ull << 60, small, st))) return rc;
-    if ((rc = launch_br(ctx, small, count, BrTv{1ull << (65 - P + b), 0, 0}, 1, nullptr, d_ct_v, nullptr, nullptr,
-                        st)))
-      return rc;
-    // bits b, b+1: top bit is now 0 -> 4-slot staircase, output D' * 2^b * Delta
-    if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 3, 1ull << 60, small, st))) return rc;
-    if ((rc = launch_br(ctx, small, count, BrTv{0, 1ull << (64 - P + b), logN - 2}, 2, nullptr, d_ct_v, nullptr,
-                        nullptr, st)))
-      return rc;
+  for (; b + d <= m; b += d)
+    if ((rc = digit(b, d))) return rc;
+  if (m - b >= 3) {
+    if ((rc = digit(b, m - b))) return rc;
+    b = m;
   }
   for (; b < m; ++b) {
     if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 1, 1ull << 62, small, st))) return rc;
@@ -1620,8 +1695,8 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
                         st)))
       return rc;
   }
-  // sign = MSB of the top digit [P-3, P)
-  if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, 0, 1ull << 60, small, st))) return rc;
+  // sign = MSB of the top digit [P-d, P)
+  if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, 0, 1ull << (63 - d), small, st))) return rc;
   return launch_br(ctx, small, count, BrTv{1ull << 62, 0, 0}, 1, nullptr, d_ct_v, nullptr, d_sign, st);
 }
 
@@ -1777,6 +1852,15 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream) {
   int rc = need_device(ctx);
   if (rc) return rc;
   HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+  return FHE_OK;
+}
+
+int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (!h_out) return fail(ctx, FHE_E_ARG, "null output");
+  HIPCHK(ctx, hipDeviceSynchronize());
+  HIPCHK(ctx, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_v4_stamps), sizeof(unsigned long long) * 64));
   return FHE_OK;
 }
 

@@ -15,7 +15,7 @@ FHE_OK = 0
 ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOMEM"}
 
 PARAM_FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
-                "lwe_noise_bits", "glwe_noise_bits", "msg_bits")
+                "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits")
 
 
 class FheParams(C.Structure):
@@ -52,7 +52,8 @@ SIGNATURES = [
     ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
     ("fhe_bit_extract_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp, _vp]),
     ("fhe_sign_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
-    ("fhe_sign_pbs_count", C.c_int, [_i32]),
+    ("fhe_sign_digit_bits", C.c_int, [_P]),
+    ("fhe_sign_pbs_count", C.c_int, [_P]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     ("fhe_quantize_pairs", C.c_int, [_CTXP, _vp, _i32, _vp, _i32, _i64, _i32, C.c_double, _i64, _i64, _i64, _vp, _vp]),
@@ -63,6 +64,7 @@ SIGNATURES = [
     ("fhe_memcpy_h2d", C.c_int, [_CTXP, _vp, _vp, C.c_size_t, _vp]),
     ("fhe_memcpy_d2h", C.c_int, [_CTXP, _vp, _vp, C.c_size_t, _vp]),
     ("fhe_stream_sync", C.c_int, [_CTXP, _vp]),
+    ("fhe_debug_v4_stamps", C.c_int, [_CTXP, _vp]),
     ("fhe_profile_enable", C.c_int, [_CTXP, C.c_int]),
     ("fhe_profile_read", C.c_int, [_CTXP, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64), C.POINTER(_i64)]),
 ]
@@ -100,4 +102,4 @@ def check(rc: int, ctx=None) -> None:
 
 
 def params_struct(d: dict) -> FheParams:
-    return FheParams(**{f: int(d[f]) for f in PARAM_FIELDS})
+    return FheParams(**{f: int(d.get(f, 0) if f == "sign_digit_bits" else d[f]) for f in PARAM_FIELDS})

@@ -55,6 +55,9 @@ typedef struct fhe_params {
   int32_t lwe_noise_bits;  /* TUniform bound, small LWE and KSK */
   int32_t glwe_noise_bits; /* TUniform bound, GLWE, BSK and big-key LWE */
   int32_t msg_bits;        /* P: message width of the accumulator encoding */
+  int32_t sign_digit_bits; /* digit width d of fhe_sign_batch (3 or 4), or 0: the
+                              widest d whose worst round keeps >= 9.2 sigma
+                              (fhe_sign_digit_bits) */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;
@@ -127,10 +130,14 @@ int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_
 
 /* Sign of the msg_bits-bit value v in d_ct_v (consumed): d_sign receives the
  * encryption of [v < 0] at 2^63 (decrypt with fhe_decrypt_bits_batch). Uses
- * fhe_sign_pbs_count(msg_bits) key switches + bootstraps per ciphertext:
- * 3-bit digits, two bootstraps each, 10 at msg_bits = 16. */
+ * fhe_sign_pbs_count(params) key switches + bootstraps per ciphertext: d-bit
+ * digits (d = fhe_sign_digit_bits), two bootstraps each, then the sign of the
+ * top d bits; 7 at msg_bits = 16 (d = 4). */
 int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, void* stream);
-int fhe_sign_pbs_count(int32_t msg_bits);
+/* Resolved digit width (params->sign_digit_bits, or the noise-model choice
+ * when it is 0); 0 for msg_bits < 4 (single-bit rounds); -1 on bad params. */
+int fhe_sign_digit_bits(const fhe_params* params);
+int fhe_sign_pbs_count(const fhe_params* params);
 /* Bootstrap with a staircase test vector over 2^log_slots slots of the half
  * torus: output phase ~ base + floor(phase * 2^log_slots / 2^63) * step for an
  * input phase in [0, 2^63) (negacyclic beyond). log_slots = 0, step = 0 is
@@ -143,7 +150,7 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
  * of the per-document loop at batch_operations.py:268-279 and of
  * compare_encrypted (batch_operations.py:206-238):
  *   encrypt q_x (B x D) -> linear with d_w and cst - T -> decrypt the
- *   leveled accumulator -> sign extraction (fhe_sign_pbs_count(msg_bits)
+ *   leveled accumulator -> sign extraction (fhe_sign_pbs_count(params)
  *   KS + PBS) -> decrypt the sign bit. d_acc[b] = the decrypted accumulator (exact int64, = Concrete's
  *   q_x @ q_w - zp*sum(q_w) + q_b; read from the leveled ciphertext like the
  *   reference's leveled circuit), d_below[b] = 1 iff acc < T (the decrypted
@@ -188,6 +195,9 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
  * processed for kernel "blind_rotate" or "keyswitch", then resets them. */
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
+/* Development aid: 4 x 16 s_memtime phase stamps of one wave of the v4 blind
+ * rotation, recorded only when FHEICP_V4_DBG=128 (tools/prof_br.py --stamps). */
+int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out);
 
 #ifdef __cplusplus
 }

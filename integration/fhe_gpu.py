@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
-          "lwe_noise_bits", "glwe_noise_bits", "msg_bits")
+          "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits")
 
 
 class fhe_params(C.Structure):

@@ -28,6 +28,7 @@
  * bootstrap, and differ there only by a small bounded phase error
  * (tests/test_gpu_parity.py checks both).
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -43,6 +44,7 @@ typedef struct {
   int32_t lwe_noise_bits;  /* TUniform bound: small LWE / KSK */
   int32_t glwe_noise_bits; /* TUniform bound: GLWE / BSK / big-key LWE */
   int32_t msg_bits;        /* P: message width */
+  int32_t sign_digit_bits; /* sign-extraction digit width, 0 = noise-model choice */
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -492,15 +494,51 @@ static void sign_round(const ref_params* P, const uint64_t* bsk, const uint64_t*
   for (int t = 0; t < Wb; ++t) cv[t] -= ob[t];
 }
 
-/* Sign of the P-bit value in ct_v with 3-bit digits (the
- * algorithm of fhe_sign_batch): clear the low m = P - 3 bits LSB-first, a
- * full digit [b, b+3) by a sign bootstrap of its top bit (v << (P-b-3),
- * centred by 2^60, tv 2^(65-P+b)) then a 4-slot staircase of its two low bits
- * (step 2^(64-P+b)); leftover bits by single-bit rounds; then the top digit's
- * MSB. sign[count x (kN+1)] encrypts [v < 0] at 2^63; ct_v is consumed. */
+/* Digit width of the sign extraction: the explicit
+ * sign_digit_bits, else d = 4 if its worst round -- margin
+ * 2^-(d+1), the previous bootstrap's variance amplified by 4^(P-d), plus the
+ * key-switch and modulus-switch variances -- keeps >= 9.2 sigma, else 3. */
+static double tu_var(int b) { return (ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
+
+static int digit_bits(const ref_params* P) {
+  if (P->msg_bits < 4) return 0;
+  if (P->sign_digit_bits) return P->sign_digit_bits < P->msg_bits ? P->sign_digit_bits : P->msg_bits;
+  const double q2 = ldexp(1.0, 128);
+  const double beta = ldexp(1.0, P->pbs_base_log), bk = ldexp(1.0, P->ks_base_log);
+  const double key = (double)P->n * P->pbs_level * (P->k + 1) * P->N * (beta * beta + 2) / 12.0 *
+                     tu_var(P->glwe_noise_bits) / q2;
+  const double rnd = (double)P->n * (1 + P->k * P->N / 2.0) / (12.0 * pow(beta, 2.0 * P->pbs_level));
+  const double ks = (double)P->k * P->N * P->ks_level * (bk * bk + 2) / 12.0 * tu_var(P->lwe_noise_bits) / q2 +
+                    P->k * P->N / 2.0 * ldexp(1.0, -2 * P->ks_level * P->ks_base_log) / 12.0;
+  const double ms = (P->n / 2.0 + 1) / 12.0 / ((2.0 * P->N) * (2.0 * P->N));
+  for (int d = P->msg_bits < 4 ? P->msg_bits : 4; d > 3; --d) {
+    const double sigma = sqrt((key + rnd) * ldexp(1.0, 2 * (P->msg_bits - d)) + ks + ms);
+    if (ldexp(1.0, -(d + 1)) / sigma >= 9.2) return d;
+  }
+  return 3;
+}
+
+/* One c-bit digit [b, b+c) of the value in cv: a sign bootstrap of its top bit
+ * (v << (P-b-c), centred by 2^(63-c), tv 2^(62-P+b+c)), then a
+ * 2^(c-1)-slot staircase of its c-1 low bits (step 2^(64-P+b)). */
+static void digit_rounds(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* cv, int b, int c,
+                         uint64_t* sh, uint64_t* sm, uint64_t* ob, uint64_t* work) {
+  const int Pb = P->msg_bits, lgN = ilog2(P->N);
+  const tv_desc hi = {1ull << (62 - Pb + b + c), 0, 0};
+  sign_round(P, bsk, ksk, cv, Pb - b - c, 1ull << (63 - c), &hi, 1, sh, sm, ob, work);
+  const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - (c - 1)};
+  sign_round(P, bsk, ksk, cv, Pb - b - c, 1ull << (63 - c), &lo, 2, sh, sm, ob, work);
+}
+
+/* Sign of the P-bit value in ct_v with d-bit digits (the
+ * algorithm of fhe_sign_batch): clear the low m = P - d bits LSB-first, full
+ * digits [b, b+d) by digit_rounds, a leftover of >= 3 bits as one shorter
+ * digit, of 1-2 bits by single-bit rounds; then the sign of the top d bits
+ * (centred by 2^(63-d), tv 2^62). sign[count x (kN+1)] encrypts [v < 0] at
+ * 2^63; ct_v is consumed. */
 void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
                       uint64_t* sign) {
-  const int Wb = P->k * P->N + 1, Pb = P->msg_bits, lgN = ilog2(P->N);
+  const int Wb = P->k * P->N + 1, Pb = P->msg_bits, d = digit_bits(P);
 #pragma omp parallel
   {
     uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
@@ -512,24 +550,23 @@ void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* 
       uint64_t* cv = ct_v + (size_t)c * Wb;
       if (Pb < 4) {
         for (int i = 0; i < Pb; ++i) {
-          const tv_desc d = {1ull << (63 - Pb + i), 0, 0};
-          sign_round(P, bsk, ksk, cv, Pb - 1 - i, 1ull << 62, &d, 1, sh, sm, ob, work);
+          const tv_desc t = {1ull << (63 - Pb + i), 0, 0};
+          sign_round(P, bsk, ksk, cv, Pb - 1 - i, 1ull << 62, &t, 1, sh, sm, ob, work);
         }
       } else {
-        const int m = Pb - 3;
+        const int m = Pb - d;
         int b = 0;
-        for (; b + 3 <= m; b += 3) {
-          const tv_desc hi = {1ull << (65 - Pb + b), 0, 0};
-          sign_round(P, bsk, ksk, cv, Pb - b - 3, 1ull << 60, &hi, 1, sh, sm, ob, work);
-          const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - 2};
-          sign_round(P, bsk, ksk, cv, Pb - b - 3, 1ull << 60, &lo, 2, sh, sm, ob, work);
+        for (; b + d <= m; b += d) digit_rounds(P, bsk, ksk, cv, b, d, sh, sm, ob, work);
+        if (m - b >= 3) {
+          digit_rounds(P, bsk, ksk, cv, b, m - b, sh, sm, ob, work);
+          b = m;
         }
         for (; b < m; ++b) {
-          const tv_desc d = {1ull << (63 - Pb + b), 0, 0};
-          sign_round(P, bsk, ksk, cv, Pb - b - 1, 1ull << 62, &d, 1, sh, sm, ob, work);
+          const tv_desc t = {1ull << (63 - Pb + b), 0, 0};
+          sign_round(P, bsk, ksk, cv, Pb - b - 1, 1ull << 62, &t, 1, sh, sm, ob, work);
         }
         const tv_desc top = {1ull << 62, 0, 0};
-        sign_round(P, bsk, ksk, cv, 0, 1ull << 60, &top, 1, sh, sm, ob, work);
+        sign_round(P, bsk, ksk, cv, 0, 1ull << (63 - d), &top, 1, sh, sm, ob, work);
       }
       memcpy(sign + (size_t)c * Wb, ob, 8 * (size_t)Wb);
     }
@@ -537,10 +574,14 @@ void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* 
   }
 }
 
-int ref_sign_pbs_count(int Pb) {
+int ref_sign_digit_bits(const ref_params* P) { return digit_bits(P); }
+
+int ref_sign_pbs_count(const ref_params* P) {
+  const int Pb = P->msg_bits, d = digit_bits(P);
   if (Pb < 1) return 0;
   if (Pb < 4) return Pb;
-  return 2 * ((Pb - 3) / 3) + (Pb - 3) % 3 + 1;
+  const int m = Pb - d, r = m % d;
+  return 2 * (m / d) + (r >= 3 ? 2 : r) + 1;
 }
 
 /* Decrypt the sign ciphertext: 1 iff phase in [2^62, 3*2^62) i.e. bit set. */

@@ -16,7 +16,7 @@ _HERE = Path(__file__).resolve().parent
 _LIB_PATH = _HERE / "build" / "libtfhe_ref.so"
 
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
-          "lwe_noise_bits", "glwe_noise_bits", "msg_bits")
+          "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits")
 
 
 class RefParams(C.Structure):
@@ -57,7 +57,8 @@ def lib():
         L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
         L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
-        L.ref_sign_pbs_count.argtypes = [C.c_int]; L.ref_sign_pbs_count.restype = C.c_int
+        L.ref_sign_pbs_count.argtypes = [P]; L.ref_sign_pbs_count.restype = C.c_int
+        L.ref_sign_digit_bits.argtypes = [P]; L.ref_sign_digit_bits.restype = C.c_int
         L.ref_negacyclic_mul.argtypes = [u64p, u64p, u64p, C.c_int]
         L.ref_decompose.argtypes = [C.c_uint64, C.c_int, C.c_int, i64p]
         L.ref_tuniform.argtypes = [C.c_uint64, C.c_int]; L.ref_tuniform.restype = C.c_int64
@@ -83,7 +84,7 @@ class RefTFHE:
     """Exact CPU TFHE with the same parameters and PRNG streams as the GPU."""
 
     def __init__(self, params: dict, seed: int):
-        self.params = {f: int(params[f]) for f in FIELDS}
+        self.params = {f: int(params.get(f, 0) if f == "sign_digit_bits" else params[f]) for f in FIELDS}
         self.P = RefParams(**self.params)
         L = lib()
         self.n, self.k, self.N = self.params["n"], self.params["k"], self.params["N"]
@@ -214,5 +215,13 @@ def chacha20_block(key_words, counter: int, nonce_words) -> np.ndarray:
     return out
 
 
-def sign_pbs_count(P: int) -> int:
-    return int(lib().ref_sign_pbs_count(int(P)))
+def _ref_params(params: dict) -> RefParams:
+    return RefParams(**{f: int(params.get(f, 0) if f == "sign_digit_bits" else params[f]) for f in FIELDS})
+
+
+def sign_digit_bits(params: dict) -> int:
+    return int(lib().ref_sign_digit_bits(C.byref(_ref_params(params))))
+
+
+def sign_pbs_count(params: dict) -> int:
+    return int(lib().ref_sign_pbs_count(C.byref(_ref_params(params))))

@@ -5,6 +5,8 @@ and every decrypted value. After a bootstrap the GPU's f64-FFT rounding
 differs from the oracle's exact Karatsuba product by a bounded phase error,
 checked against a tolerance well inside the decision margin.
 """
+from dataclasses import replace
+
 import numpy as np
 import pytest
 import torch
@@ -188,25 +190,33 @@ def test_bit_extract_real_params_other_kernels(need_gpu, oracle_lib, monkeypatch
     assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
 
 
-def test_sign_toy_all_values_vs_oracle(toy):
-    """Digit sign extraction (fhe_sign_batch): every toy value, and the GPU
+@pytest.mark.parametrize("P,dbits", [(8, 3), (8, 4), (7, 4), (5, 4), (4, 4)])
+def test_sign_toy_all_values_vs_oracle(need_gpu, oracle_lib, P, dbits):
+    """Digit sign extraction (fhe_sign_batch) with 3- and 4-bit digits: every
+    toy value, each branch shape (full digits, a 3-bit leftover digit at P=7,
+    a single leftover bit at P=5, the top chunk alone at P=4), and the GPU
     sign ciphertexts' phases track the oracle's restatement."""
-    eng, ref = toy
-    P = eng.msg_bits
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=dbits)
+    eng = Engine(prm, 0)
+    eng.keygen(1234)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 1234)
     v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
     sign = eng.sign(eng.encrypt(v, seed=41))
     assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
-    sel = np.array([0, 1, 127, 128, 129, 255])
+    h = 2 ** (P - 1)
+    sel = np.array([0, 1, h - 1, h, h + 1, 2 * h - 1])
     s_ref = ref.sign_extract(ref.encrypt_ints(v[sel], seed=41, id0=0))
     assert np.array_equal(ref.decrypt_bits(s_ref), (v[sel] < 0).astype(np.int64))
     d = signed(u64(eng.phase(sign[sel].contiguous())) - ref.phase(s_ref))
     assert np.abs(d).max() < 2 ** 56
+    eng.close()
 
 
-@pytest.mark.parametrize("P", [16, 21])
-def test_sign_real_params(need_gpu, P):
-    """Real parameters at the C2/C4 (P=16) and C3 (P=21) widths, boundaries included."""
-    eng = Engine(params_for_bits(P), 0)
+@pytest.mark.parametrize("P,dbits", [(16, 0), (16, 3), (21, 0)])
+def test_sign_real_params(need_gpu, P, dbits):
+    """Real parameters at the C2/C4 (P=16: 4-bit digits, and 3-bit forced)
+    and C3 (P=21: 3-bit) widths, boundaries included."""
+    eng = Engine(replace(params_for_bits(P), sign_digit_bits=dbits), 0)
     eng.keygen(900 + P)
     rng = np.random.default_rng(P)
     h = 2 ** (P - 1)

@@ -127,11 +127,15 @@ def test_real_params_roundtrip(oracle_lib):
     assert np.abs(err).max() < 2 ** 58
 
 
-@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8])
-def test_sign_extract_digits_all_values(toy_ref, P):
-    """The 3-bit digit sign algorithm (fhe_sign_batch) on every P-bit value,
-    covering each branch shape: P < 4, full digits, leftover single bits."""
+@pytest.mark.parametrize("d", [3, 4])
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_sign_extract_digits_all_values(toy_ref, P, d):
+    """The d-bit digit sign algorithm (fhe_sign_batch) on every P-bit value,
+    covering each branch shape: P < 4, full digits, a 3-bit leftover digit
+    (d = 4, P = 7), leftover single bits, top chunk only (d = 4, P = 4)."""
     r = toy_ref.with_msg_bits(P)
+    r.params["sign_digit_bits"] = d
+    r.P = type(r.P)(**r.params)
     v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
     sign = r.sign_extract(r.encrypt_ints(v, seed=100 + P))
     assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
@@ -139,8 +143,13 @@ def test_sign_extract_digits_all_values(toy_ref, P):
 
 def test_sign_pbs_count(oracle_lib):
     from oracle.tfhe_ref import sign_pbs_count
-    want = {1: 1, 2: 2, 3: 3, 4: 2, 6: 3, 7: 4, 8: 5, 9: 5, 16: 10, 21: 13, 26: 17}
-    assert {P: sign_pbs_count(P) for P in want} == want
+    from fheicp.params import params_for_bits
+    # 4-bit digits where the noise bar allows them (P <= 16 here), else 3-bit
+    want = {1: 1, 2: 2, 3: 3, 4: 1, 6: 3, 7: 3, 8: 3, 9: 4, 16: 7, 17: 11, 21: 13, 26: 17}
+    assert {P: sign_pbs_count(params_for_bits(P).as_dict()) for P in want} == want
+    want3 = {4: 2, 6: 3, 7: 4, 8: 5, 9: 5, 16: 10, 21: 13, 26: 17}
+    got3 = {P: sign_pbs_count({**params_for_bits(P).as_dict(), "sign_digit_bits": 3}) for P in want3}
+    assert got3 == want3
 
 
 def test_pbs_lut_staircase(toy_ref):

@@ -8,7 +8,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from fheicp.params import PBS_GADGETS, params_for_bits, noise_report, sign_pbs_count
+from fheicp.params import PBS_GADGETS, TOY, params_for_bits, noise_report, sign_digit_bits, sign_pbs_count
 from fheicp.search import sharded_topk
 
 
@@ -27,10 +27,34 @@ def test_gadget_table_has_margin(pmax, beta, lvl):
         assert noise_report(p.with_msg_bits(pmax + 1))["margin_sigmas"] < 9.2
 
 
-def test_sign_pbs_count_matches_oracle(oracle_lib):
-    for P in range(1, 28):
-        assert sign_pbs_count(P) == oracle_lib.sign_pbs_count(P)
-    assert sign_pbs_count(16) == 10
+def _param_sets():
+    for P in range(2, 28):
+        p = params_for_bits(P)
+        for d in (0, 3, 4):
+            yield p.with_msg_bits(P).__class__(**{**p.as_dict(), "sign_digit_bits": d})
+    for P in range(2, 17):
+        yield TOY.with_msg_bits(P)
+
+
+def test_sign_digits_match_oracle_and_library(oracle_lib):
+    """Digit width and PBS count: params.py, the C library (host-only call) and
+    the oracle restatement resolve every parameter set identically."""
+    from fheicp import _lib
+    L = _lib.lib()
+    for p in _param_sets():
+        d = p.as_dict()
+        cp = _lib.params_struct(d)
+        assert sign_digit_bits(p) == oracle_lib.sign_digit_bits(d) == L.fhe_sign_digit_bits(cp), d
+        assert sign_pbs_count(p) == oracle_lib.sign_pbs_count(d) == L.fhe_sign_pbs_count(cp), d
+    # the headline width: 4-bit digits at P = 16, 3-bit where 4 misses the bar
+    assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 3, 3, 3]
+    assert sign_pbs_count(16) == 7
+    assert noise_report(params_for_bits(16))["digit_bits"] == 4
+
+
+def test_sign_digit_bits_validation():
+    with pytest.raises(ValueError):
+        sign_digit_bits(params_for_bits(16).__class__(sign_digit_bits=5))
 
 
 def test_params_for_bits_limits():

@@ -20,9 +20,12 @@ ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--P", type=int, default=16)
 ap.add_argument("--variants", default="4,2")
 ap.add_argument("--dbg", default="", help="comma list of FHEICP_V4_DBG values to time (v4 only; wrong results)")
+ap.add_argument("--stamps", action="store_true", help="print v4 phase timestamps (FHEICP_V4_DBG=128)")
 a = ap.parse_args()
 import os
 runs = [(v, "0") for v in a.variants.split(",")] + [("4", d) for d in a.dbg.split(",") if d]
+if a.stamps:
+    runs.append(("4", "128"))
 for var, dbg in runs:
     os.environ["FHEICP_BR_VARIANT"] = var
     os.environ["FHEICP_V4_DBG"] = dbg
@@ -37,6 +40,16 @@ for var, dbg in runs:
     torch.cuda.synchronize()
     br = eng.profile_read("blind_rotate")
     ks = eng.profile_read("keyswitch")
+    if dbg == "128":
+        import ctypes as C
+        st = np.zeros(64, np.uint64)
+        eng._chk(eng._L.fhe_debug_v4_stamps(eng._ctx, C.c_void_p(st.ctypes.data)))
+        names = ["start", "digits", "fwd0", "F0+mac0", "bar1", "mac0x", "bar2", "fwd1", "F1+mac1", "bar3",
+                 "mac1x", "bar4", "inverse", "acc"]
+        for s4 in range(4):
+            row = st[s4 * 16:s4 * 16 + 14].astype(np.int64)
+            d = np.diff(row)
+            print("step", 100 + s4, "total", int(row[-1] - row[0]), " ".join(f"{n}:{int(x)}" for n, x in zip(names[1:], d)))
     print(f"variant={var} dbg={dbg} B={a.B} blind_rotate {br['total_ms'] / br['launches']:.3f} ms/launch "
           f"({a.B * br['launches'] / br['total_ms'] * 1e3:.0f} PBS/s), keyswitch {ks['total_ms'] / ks['launches']:.3f} ms/launch")
     eng.close()

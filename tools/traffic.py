@@ -13,18 +13,19 @@ import sys
 
 
 def per_launch(path, counter, match="k_blind_rotate"):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if match in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    if not vals:
+    rows = [r for r in csv.DictReader(open(path)) if match in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    if not rows:
         raise SystemExit(f"no {counter} rows for {match} in {path}")
-    return sum(vals) / len(vals), len(vals)
+    vals = [float(r["Counter_Value"]) for r in rows]
+    names = sorted({r["Kernel_Name"].split("(")[0] for r in rows})
+    return sum(vals) / len(vals), len(vals), names
 
 
 def main():
-    fetch, nf = per_launch(sys.argv[1], "FETCH_SIZE")
-    write, nw = per_launch(sys.argv[2], "WRITE_SIZE")
+    fetch, nf, names = per_launch(sys.argv[1], "FETCH_SIZE")
+    write, nw, _ = per_launch(sys.argv[2], "WRITE_SIZE")
     out = {
-        "kernel": "k_blind_rotate_mw<V2>",
+        "kernel": ", ".join(names),
         "fetch_size_kib_raw": fetch,
         "write_size_kib": write,
         "launches": [nf, nw],
