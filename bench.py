@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-compares", type=int, default=16)
+    ap.add_argument("--mode", choices=("compare", "corpus"), default="compare",
+                    help="compare: the reference's path (configs[1]); corpus: search over a stored corpus of "
+                         "seeded-LWE documents (SURVEY.md §8f-1)")
     return ap.parse_args()
 
 
@@ -103,6 +106,46 @@ def br_flops_per_ct(p) -> float:
     return p.n * (nf * fft + ni * fft + pointwise)
 
 
+def roofline(p, br) -> dict:
+    """External-product (blind rotation) kernel roofline from the HIP events
+    bracketing every launch on its stream (fhe_profile_read)."""
+    avg_ms = br["total_ms"] / max(br["launches"], 1)
+    cts_per_launch = br["items"] / max(br["launches"], 1)
+    R = (p.k + 1) * p.pbs_level
+    bsk_bytes = p.n * R * (p.k + 1) * (p.N // 2) * 16
+    io_bytes = cts_per_launch * ((p.n + 1) * 8 + (p.k * p.N + 1) * 8 * 5)
+    alg_bytes = bsk_bytes + io_bytes
+    achieved_gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
+    flops = br_flops_per_ct(p) * cts_per_launch
+    achieved_tf = flops / (avg_ms * 1e-3) / 1e12
+    traffic = None
+    tj = REPO / "profiles" / "r01_br_traffic.json"
+    if tj.exists():
+        try:
+            tr = json.loads(tj.read_text())
+            if tr.get("pbs_level", p.pbs_level) == p.pbs_level:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {
+        "kernel": "k_blind_rotate (external products)",
+        "bound": "hbm",
+        "achieved": round(achieved_gbs, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+        "traffic": traffic,
+        "avg_launch_ms": round(avg_ms, 4),
+        "launches": br["launches"],
+        "cts_per_launch": cts_per_launch,
+        "alg_bytes_per_launch": int(alg_bytes),
+        "note": "algorithmic bytes = FFT-domain BSK once per launch + per-ct LWE I/O; the kernel is f64-VALU "
+                "bound, see compute",
+        "compute": {"achieved_tflops_f64": round(achieved_tf, 2), "peak_tflops_f64": F64_VALU_PEAK_TFLOPS,
+                    "frac": round(achieved_tf / F64_VALU_PEAK_TFLOPS, 4)},
+    }
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -110,6 +153,8 @@ def main():
     torch.cuda.set_device(dev)
     from fheicp import _lib
     _lib.lib()  # loud failure if the HIP library is missing
+    if args.mode == "corpus":
+        return corpus_main(args, world, rank, local, dev)
 
     model = build_model(args)
     model.compile(key_seed=args.seed, device=local)
@@ -163,23 +208,7 @@ def main():
     value = compares / elapsed
     ms_step = elapsed / args.steps * 1e3
 
-    # external-product (blind rotation) kernel roofline, from HIP events
-    avg_ms = br["total_ms"] / max(br["launches"], 1)
-    cts_per_launch = br["items"] / max(br["launches"], 1)
-    R = (p.k + 1) * p.pbs_level
-    bsk_bytes = p.n * R * (p.k + 1) * (p.N // 2) * 16
-    io_bytes = cts_per_launch * ((p.n + 1) * 8 + (p.k * p.N + 1) * 8 * 5)
-    alg_bytes = bsk_bytes + io_bytes
-    achieved_gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
-    flops = br_flops_per_ct(p) * cts_per_launch
-    achieved_tf = flops / (avg_ms * 1e-3) / 1e12
-    traffic = None
-    tj = REPO / "profiles" / "r01_br_traffic.json"
-    if tj.exists():
-        try:
-            traffic = json.loads(tj.read_text()).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    roof = roofline(p, br)
 
     out = {
         "metric": METRIC,
@@ -203,23 +232,7 @@ def main():
             "params": p.as_dict(), "parallelism": f"shard{world}",
         },
         "pbs_per_sec": round(value * n_pbs, 1),
-        "roofline": {
-            "kernel": "k_blind_rotate (external products)",
-            "bound": "hbm",
-            "achieved": round(achieved_gbs, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
-            "traffic": traffic,
-            "avg_launch_ms": round(avg_ms, 4),
-            "launches": br["launches"],
-            "cts_per_launch": cts_per_launch,
-            "alg_bytes_per_launch": int(alg_bytes),
-            "note": "algorithmic bytes = FFT-domain BSK once per launch + per-ct LWE I/O; the kernel is f64-VALU "
-                    "bound, see compute",
-            "compute": {"achieved_tflops_f64": round(achieved_tf, 2), "peak_tflops_f64": F64_VALU_PEAK_TFLOPS,
-                        "frac": round(achieved_tf / F64_VALU_PEAK_TFLOPS, 4)},
-        },
+        "roofline": roof,
         "keyswitch_ms_total": round(ks["total_ms"], 3),
     }
 
@@ -307,6 +320,129 @@ def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
     t_clear = (time.perf_counter() - t0) / reps
     base["clear_path_compares_per_s"] = round(len(Xp) / t_clear, 1)
     return base, parity
+
+
+def corpus_main(args, world, rank, local, dev):
+    """--mode corpus: one query against a stored corpus of encrypted
+    documents (fheicp.corpus). The documents are encrypted
+    before the timed region (they are persisted ciphertexts) and resident in
+    HBM as seeded LWEs (D body words + 1 stream id per document). One step =
+    query plan (host, D values) -> seeded linear (masks regenerated in
+    registers) -> decrypt -> sign extraction -> decrypt bit -> top-k (+ the
+    RCCL all-gather for N > 1)."""
+    from fheicp.corpus import CorpusQuant, EncryptedCorpus
+    from fheicp.datagen import training_embeddings
+    from fheicp.params import sign_pbs_count
+    from fheicp.search import sharded_topk
+    model = build_model(args)
+    e1, e2 = training_embeddings(args.dim, 1000, seed=args.seed + 1)
+    cq = CorpusQuant.calibrate(model.qparams, np.concatenate([e1, e2]))
+    c = EncryptedCorpus(cq).compile(key_seed=args.seed, device=local, noise_seed=args.seed + 7)
+    eng = c.engine
+    q_np, docs_np = shard(args, rank)
+    B = docs_np.shape[0]
+    base_idx = rank * B
+    ids = (np.arange(B, dtype=np.uint64) + np.uint64(base_idx)) * np.uint64(args.dim)
+    bodies, ids = c.encrypt_docs(docs_np, ids)
+    bd = torch.from_numpy(bodies.view(np.int64)).to(dev)
+    idd = torch.from_numpy(ids.view(np.int64)).to(dev)
+    _, _, _, P = c.query_plan(q_np, args.min_similarity)
+    p = eng.params.with_msg_bits(P)
+    n_pbs = sign_pbs_count(p)
+
+    def step():
+        acc, below, _ = c.compare(bd, idd, q_np, args.min_similarity)
+        oa, oi = sharded_topk(acc, below, args.top_k, base_idx, eng.topk, world)
+        return acc, below, oa, oi
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        acc, below, oa, oi = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.profile(False)
+    br = eng.profile_read("blind_rotate")
+    ks = eng.profile_read("keyswitch")
+    if world > 1:
+        on_dev = torch.distributed.get_backend() == "nccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if on_dev else "cpu")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * B * args.steps / elapsed
+    out = {
+        "metric": METRIC + " [encrypted-corpus mode]",
+        "value": round(value, 2), "unit": "compares/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {
+            "workload": f"search 1 clear query x {B} stored encrypted docs (seeded LWE) per GPU, {args.dim}-dim, "
+                        f"n_bits={args.n_bits}, bilinear quantisation (DESIGN.md §7.1) + encrypted threshold "
+                        f"(min_similarity {args.min_similarity}) + top-{args.top_k}",
+            "docs_per_gpu": B, "dim": args.dim, "n_bits": args.n_bits, "n_e": cq.n_e, "P0": c.P0,
+            "msg_bits_P": P, "pbs_per_compare": n_pbs, "keyswitch_per_compare": n_pbs,
+            "corpus_bytes_per_doc": 8 * (args.dim + 1), "params": p.as_dict(), "parallelism": f"shard{world}",
+        },
+        "pbs_per_sec": round(value * n_pbs, 1),
+        "roofline": roofline(p, br),
+        "keyswitch_ms_total": round(ks["total_ms"], 3),
+    }
+    if rank == 0:
+        from oracle import quant_ref as Q
+        X, y = __import__("fheicp.datagen", fromlist=["x"]).training_pairs(args.dim, 1000, seed=args.seed + 1)
+        oq = Q.fit_quantized_linear(X, y, args.n_bits)
+        all_docs = np.concatenate([shard(args, r)[1] for r in range(world)])
+        want = Q.corpus_search(oq, cq.s_e, cq.n_e, q_np, all_docs, args.top_k, args.min_similarity)
+        s = np.float64(cq.out_scale)
+        got = [(int(i), float(s * np.float64(a))) for a, i in zip(oa.cpu().tolist(), oi.cpu().tolist()) if i >= 0]
+        ref_acc = Q.corpus_accumulate(oq, cq.s_e, cq.n_e, q_np, docs_np)
+        sc = s * ref_acc.astype(np.float64)
+        out["parity"] = {
+            "compares_checked": B,
+            "acc_bit_exact": bool(np.array_equal(acc.cpu().numpy(), ref_acc)),
+            "threshold_bit_exact": bool(np.array_equal(below.cpu().numpy(), (sc < args.min_similarity).astype(np.int64))),
+            "topk_equal": got == want,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = corpus_cpu_leg(args, c, bodies, ids, oq, cq, q_np, docs_np, P, out["parity"])
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def corpus_cpu_leg(args, c, bodies, ids, oq, cq, q_np, docs_np, P, parity):
+    """The exact C oracle on a bounded sample of the corpus workload: expand
+    the seeded documents, linear, decrypt, sign extraction, decrypt."""
+    from oracle import quant_ref as Q
+    from oracle import tfhe_ref as R
+    Cn = args.cpu_compares
+    p0 = c.scheme.as_dict()
+    ref = R.RefTFHE(p0, args.seed)
+    Wr, cst, T, P = c.query_plan(q_np, args.min_similarity)
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    ct = ref.expand_seeded(bodies[:Cn], ids[:Cn], c.mask_key)
+    ref.with_msg_bits(P)
+    lin = ref.linear(ct, Cn, args.dim, Wr, cst - T)
+    v = ref.decrypt_ints(lin)
+    bits = ref.decrypt_bits(ref.sign_extract(lin))
+    t_total = time.perf_counter() - t0
+    acc_ref = Q.corpus_accumulate(oq, cq.s_e, cq.n_e, q_np, docs_np[:Cn])
+    parity["cpu_oracle_acc_matches"] = bool(np.array_equal(v + T, acc_ref))
+    parity["cpu_oracle_threshold_matches"] = bool(np.array_equal(bits, (acc_ref < T).astype(np.int64)))
+    return {"value": round(Cn / t_total, 4), "unit": "compares/s", "cores": cores, "kind": "port",
+            "sample": f"{Cn} compares of the same corpus workload on the exact C oracle (OpenMP {cores} threads): "
+                      f"expand seeded docs + linear + decrypt + {R.sign_pbs_count(dict(p0, msg_bits=P))} KS+PBS "
+                      f"sign extraction + decrypt",
+            "seconds": round(t_total, 2)}
 
 
 if __name__ == "__main__":

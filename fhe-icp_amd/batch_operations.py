@@ -59,6 +59,13 @@ class BatchConfig:
     seed: Optional[int] = None      # training-data seed when no model_path
     key_seed: Optional[int] = None  # keygen seed (None: os.urandom)
     search_chunk: int = 1 << 16     # pairs per fused GPU launch sequence
+    # encrypted-corpus mode (§8f-1, fheicp.corpus): documents are stored as
+    # seeded LWE ciphertexts and searched without decryption (bilinear
+    # quantisation; opt-in because its scores differ from the reference's)
+    store_ciphertexts: bool = False
+    embedding_bits: Optional[int] = None     # n_e (default: n_bits)
+    embedding_scale: Optional[float] = None  # s_e (default: calibrated on training embeddings)
+    corpus_path: Optional[str] = None        # fheicp.persist corpus file: load, or save after creation
 
     def __post_init__(self):
         if self.batch_size < 1:
@@ -83,9 +90,13 @@ class BatchProcessor:
         if self.config.input_dim not in (EncryptedDocument.allowed_dims or (self.config.input_dim,)):
             EncryptedDocument.allowed_dims = tuple(sorted(set(DEFAULT_DIMS) | {self.config.input_dim}))
         self._resident = None  # (host array identity, device tensor)
+        self._resident_ct = None  # (host bodies, rank range, (device bodies, device ids))
+        self.corpus_engine = None  # fheicp.corpus.EncryptedCorpus (store_ciphertexts)
         self.fhe_model = fhe_model
         if self.fhe_model is None:
             self._init_model()
+        elif self.config.store_ciphertexts and self.config.fhe == "execute":
+            self._init_corpus(self.fhe_model)
         self.initial_memory = self._check_memory()
 
     # ------------------------------------------------------------- model --
@@ -116,6 +127,27 @@ class BatchProcessor:
             if needs_keys:
                 m.compile(X[:10], key_seed=cfg.key_seed)
         self.fhe_model = m
+        if cfg.store_ciphertexts and needs_keys:
+            self._init_corpus(m)
+
+    def _init_corpus(self, m):
+        """Load (config.corpus_path) or create the encrypted-corpus engine."""
+        from fheicp import persist
+        from fheicp.corpus import CorpusQuant, EncryptedCorpus
+        cfg = self.config
+        if cfg.corpus_path and os.path.exists(cfg.corpus_path):
+            self.corpus_engine = persist.load_corpus(cfg.corpus_path, device=cfg.device)
+            return
+        qp = m.model.quant_params
+        if cfg.embedding_scale is not None:
+            cq = CorpusQuant(qp, int(cfg.embedding_bits or qp.n_bits), float(cfg.embedding_scale))
+        else:
+            from fheicp.datagen import training_embeddings
+            e1, e2 = training_embeddings(len(qp.coef), 1000, seed=0 if cfg.seed is None else cfg.seed)
+            cq = CorpusQuant.calibrate(qp, np.concatenate([e1, e2]), cfg.embedding_bits)
+        self.corpus_engine = EncryptedCorpus(cq).compile(key_seed=cfg.key_seed, device=cfg.device)
+        if cfg.corpus_path:
+            persist.save_corpus(cfg.corpus_path, self.corpus_engine)
 
     def _require_model(self) -> FHESimilarityModel:
         if self.fhe_model is None:
@@ -171,21 +203,72 @@ class BatchProcessor:
             if self._check_memory() > self.config.max_memory_mb:
                 self._maybe_gc()
             vecs = self._embed(texts[s:e])
-            docs = [EncryptedDocument(doc_id=doc_ids[i], content_hash=hashlib.sha256(texts[i].encode()).hexdigest(),
-                                      timestamp=datetime.now().isoformat(),
-                                      encrypted_embedding=np.asarray(vecs[i - s]).astype(np.float32),
-                                      key_id=key_id, metadata=metadata[i]) for i in range(s, e)]
+            docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs, key_id, metadata[s:e])
             self.storage.save_many(docs)
             out.extend(d.doc_id for d in docs)
             if (s + self.config.batch_size) % self.config.checkpoint_interval == 0:
                 self._maybe_gc()
         return out
 
+    def _make_documents(self, texts, doc_ids, vecs, key_id, metadata) -> List[EncryptedDocument]:
+        """Plaintext vectors as in the reference (:175-178), or, with
+        store_ciphertexts, seeded-LWE payloads of the quantized vectors."""
+        vecs = np.asarray(vecs).astype(np.float32)
+        if self.corpus_engine is not None:
+            from fheicp.corpus import PAYLOAD_VERSION
+            bodies, ids = self.corpus_engine.encrypt_docs(vecs)
+            payloads = self.corpus_engine.payloads(bodies, ids)
+            version = PAYLOAD_VERSION
+        else:
+            payloads, version = list(vecs), "1.0"
+        stamp = datetime.now().isoformat()
+        return [EncryptedDocument(doc_id=doc_ids[i], content_hash=hashlib.sha256(texts[i].encode()).hexdigest(),
+                                  timestamp=stamp, encrypted_embedding=payloads[i], model_version=version,
+                                  key_id=key_id, metadata=metadata[i]) for i in range(len(doc_ids))]
+
+    def store_vectors(self, vecs: np.ndarray, doc_ids: List[str], texts: Optional[List[str]] = None,
+                      metadata: Optional[List[Dict]] = None) -> List[str]:
+        """encrypt_documents for already reduced vectors (no embedder needed)."""
+        self._require_model()
+        n = len(doc_ids)
+        texts = texts if texts is not None else list(doc_ids)
+        metadata = metadata if metadata is not None else [{} for _ in range(n)]
+        key_id = self.key_manager.get_current_key() if self.key_manager is not None else None
+        out: List[str] = []
+        for s in range(0, n, self.config.batch_size):
+            e = min(n, s + self.config.batch_size)
+            docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs[s:e], key_id, metadata[s:e])
+            self.storage.save_many(docs)
+            out.extend(d.doc_id for d in docs)
+        return out
+
     def compare_encrypted(self, doc_id1: str, doc_id2: str) -> float:
         self._require_model()
-        a = self.storage.load(doc_id1).encrypted_embedding
-        b = self.storage.load(doc_id2).encrypted_embedding
+        d1, d2 = self.storage.load(doc_id1), self.storage.load(doc_id2)
+        if self.storage.holds_ciphertexts() or d1.model_version != "1.0" or d2.model_version != "1.0":
+            return self._compare_ciphertexts(d1, d2)
+        a, b = d1.encrypted_embedding, d2.encrypted_embedding
         return float(self._predict((a * b).reshape(1, -1))[0])
+
+    def _compare_ciphertexts(self, d1, d2) -> float:
+        """Two stored ciphertexts: the key holder decrypts the first (the
+        reference's single-party trust model) and runs it as the clear query
+        against the second, which stays encrypted."""
+        import torch
+        from fheicp.corpus import unpack_payload
+        c = self.corpus_engine
+        if c is None:
+            raise RuntimeError("ciphertext documents need BatchConfig(store_ciphertexts=True, fhe='execute')")
+        p1, p2 = unpack_payload(d1.encrypted_embedding), unpack_payload(d2.encrypted_embedding)
+        c.check_payload(p1)
+        c.check_payload(p2)
+        dq1 = c.decrypt_docs(p1["body"][None, :], [p1["id0"]])[0]
+        query = np.float64(c.cq.s_e) * dq1.astype(np.float64)
+        dev = c.engine.device
+        body = torch.from_numpy(p2["body"][None, :].view(np.int64)).to(dev)
+        ids = torch.from_numpy(np.array([p2["id0"]], np.uint64).view(np.int64)).to(dev)
+        acc, _, _ = c.compare(body, ids, query, None)
+        return float(c.scores(acc.cpu().numpy())[0])
 
     # ------------------------------------------------------------ search --
     def search_similar(self, query_text: str, top_k: int = 5, min_similarity: float = 0.5) -> List[Tuple[str, float]]:
@@ -199,6 +282,8 @@ class BatchProcessor:
     def search_vector(self, query: np.ndarray, top_k: int = 5, min_similarity: float = 0.5) -> List[Tuple[str, float]]:
         """Top-k documents with score >= min_similarity for a reduced query vector."""
         m = self._require_model()
+        if self.storage.holds_ciphertexts():
+            return self._search_ciphertexts(query, top_k, min_similarity)
         ids, E = self.storage.corpus()
         if not ids:
             return []
@@ -214,6 +299,55 @@ class BatchProcessor:
             hits = self._search_gpu(m, query, E, k, min_similarity)
         out = [(ids[i], s) for i, s in hits]
         return out[:top_k]
+
+    def _search_ciphertexts(self, query, top_k: int, t: float) -> List[Tuple[str, float]]:
+        """Search over a store of seeded-LWE documents (fheicp.corpus): the
+        corpus stays encrypted in HBM (one body word per feature); every rank
+        of a torch.distributed group takes a contiguous range and the per-rank
+        top-k meet in one all-gather, as in _search_gpu."""
+        import torch
+        from fheicp.search import sharded_topk
+        c = self.corpus_engine
+        if c is None:
+            raise RuntimeError("ciphertext documents need BatchConfig(store_ciphertexts=True, fhe='execute')")
+        ids, bodies, id0, head = self.storage.encrypted_corpus()
+        if not ids:
+            return []
+        c.check_payload(head)
+        query = np.asarray(query)
+        if query.shape != (bodies.shape[1],):
+            raise ValueError(f"query shape {query.shape} does not match corpus width {bodies.shape[1]}")
+        k = len(ids) if top_k < 0 else min(int(top_k), len(ids))
+        if k == 0:
+            return []
+        dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        world = torch.distributed.get_world_size() if dist else 1
+        rank = torch.distributed.get_rank() if dist else 0
+        n = len(ids)
+        lo, hi = rank * n // world, (rank + 1) * n // world
+        eng = c.engine
+        r = self._resident_ct
+        if r is None or r[0] is not bodies or r[1] != (lo, hi):
+            r = self._resident_ct = (bodies, (lo, hi), (
+                torch.from_numpy(np.ascontiguousarray(bodies[lo:hi]).view(np.int64)).to(eng.device),
+                torch.from_numpy(np.ascontiguousarray(id0[lo:hi]).view(np.int64)).to(eng.device)))
+        bd, idd = r[2]
+        accs, belows = [], []
+        for s in range(0, hi - lo, self.config.search_chunk):
+            e = min(hi - lo, s + self.config.search_chunk)
+            acc, below, _ = c.compare(bd[s:e], idd[s:e], query, t)
+            accs.append(acc)
+            belows.append(below)
+        if accs:
+            acc, below = torch.cat(accs), torch.cat(belows)
+        else:
+            acc = torch.zeros(0, dtype=torch.int64, device=eng.device)
+            below = torch.zeros(0, dtype=torch.int64, device=eng.device)
+        oa, oi = sharded_topk(acc, below, k, lo, lambda a, b, kk, base: eng.topk(a, b, kk, base), world)
+        oa, oi = oa.cpu().numpy(), oi.cpu().numpy()
+        s = np.float64(c.cq.out_scale)
+        hits = [(ids[int(i)], float(s * np.float64(a))) for a, i in zip(oa, oi) if i >= 0]
+        return hits[:top_k]
 
     @staticmethod
     def _search_clear(m, query, E, t):

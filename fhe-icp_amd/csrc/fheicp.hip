@@ -210,6 +210,80 @@ __global__ void __launch_bounds__(256) k_encrypt(ChaKey K, int dim, int msg_bits
   }
 }
 
+// ---- seeded (compressed) ciphertexts: the stored document corpus ----------
+// A seeded LWE keeps only its body; the mask is stream(TAG_ENC_MASK, id) of
+// a PUBLIC mask key Km, the noise stream(TAG_ENC_NOISE, id) of a SECRET
+// noise key Kn. Document b of a corpus holds D bodies,
+// feature j under stream id id0[b] + j. 2049 -> 1 word per feature in HBM:
+// the masks are regenerated where they are consumed (k_linear_seeded).
+__global__ void __launch_bounds__(256) k_encrypt_seeded(ChaKey Km, ChaKey Kn, int dim, int msg_bits, int noise_bits,
+                                                        const u64* __restrict__ s_big,
+                                                        const int64_t* __restrict__ msg,
+                                                        const u64* __restrict__ id0, int D, u64* __restrict__ body) {
+  __shared__ u64 red[4];
+  const int64_t c = blockIdx.x;
+  const int64_t b = c / D;
+  const u64 id = id0[b] + (u64)(c - b * D);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 w[8];
+    stream_block(Km, TAG_ENC_MASK, id, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) part += w[q] & (0 - s_big[8 * blk + q]);
+  }
+  const u64 s = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    const u64 e = (u64)tuniform(stream_word(Kn, TAG_ENC_NOISE, id, 0), noise_bits);
+    body[c] = s + e + ((u64)msg[c] << (64 - msg_bits));
+  }
+}
+
+// full ciphertexts [B*D][dim+1] from the seeded corpus (interop / tests)
+__global__ void __launch_bounds__(256) k_expand_seeded(ChaKey Km, int dim, const u64* __restrict__ body,
+                                                       const u64* __restrict__ id0, int D, u64* __restrict__ ct) {
+  const int64_t c = blockIdx.x;
+  const int64_t b = c / D;
+  const u64 id = id0[b] + (u64)(c - b * D);
+  u64* o = ct + (size_t)c * (dim + 1);
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 w[8];
+    stream_block(Km, TAG_ENC_MASK, id, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[8 * blk + q] = w[q];
+  }
+  if (threadIdx.x == 0) o[dim] = body[c];
+}
+
+// out[b] = sum_j w[j] * ct(b, j) + cst * Delta on the seeded corpus: one
+// workgroup per document, each thread owns one 8-word ChaCha block of the
+// mask (dim / 8 threads), regenerated per feature in registers. Reads D + 1
+// words per document from HBM instead of D (dim + 1).
+__global__ void __launch_bounds__(256) k_linear_seeded(ChaKey Km, int dim, const u64* __restrict__ body,
+                                                       const u64* __restrict__ id0, int D,
+                                                       const int64_t* __restrict__ w, u64 cst_scaled,
+                                                       u64* __restrict__ out) {
+  const int64_t b = blockIdx.x;
+  const u64 base = id0[b];
+  u64* o = out + (size_t)b * (dim + 1);
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < D; ++j) {
+      u64 m[8];
+      stream_block(Km, TAG_ENC_MASK, base + (u64)j, (uint32_t)blk, m);
+      const u64 wj = (u64)w[j];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * m[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[8 * blk + q] = acc[q];
+  }
+  if (threadIdx.x == 0) {
+    u64 acc = cst_scaled;
+    for (int j = 0; j < D; ++j) acc += (u64)w[j] * body[(size_t)b * D + j];
+    o[dim] = acc;
+  }
+}
+
 // mode 0: decode signed msg_bits integer; 1: bit (nearer 2^63); 2: raw phase
 __global__ void __launch_bounds__(256) k_decrypt(int dim, int msg_bits, int mode, const u64* __restrict__ s,
                                                  const u64* __restrict__ ct, int64_t* __restrict__ out) {
@@ -1418,6 +1492,61 @@ int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_
   return FHE_OK;
 }
 
+static int seeded_args(fhe_ctx* ctx, int64_t B, int32_t D, const void* a, const void* b, const void* c) {
+  if (B < 0 || D <= 0 || (B > 0 && (!a || !b || !c))) return fail(ctx, FHE_E_ARG, "bad seeded-corpus arguments");
+  if (B * (int64_t)D > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "seeded corpus batch too large (B*D >= 2^31)");
+  return FHE_OK;
+}
+
+int fhe_encrypt_seeded_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t B, int32_t D, const uint32_t h_mask_key[8],
+                             const uint32_t h_noise_key[8], const uint64_t* d_id0, uint64_t* d_body, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if ((rc = seeded_args(ctx, B, D, d_msg, d_id0, d_body))) return rc;
+  if (!h_mask_key || !h_noise_key) return fail(ctx, FHE_E_ARG, "seeded encryption needs both keys");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  ChaKey Km, Kn;
+  for (int i = 0; i < 8; ++i) Km.w[i] = h_mask_key[i], Kn.w[i] = h_noise_key[i];
+  hipLaunchKernelGGL(k_encrypt_seeded, dim3((unsigned)(B * D)), dim3(256), 0, (hipStream_t)stream, Km, Kn, p.k * p.N,
+                     p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_msg, d_id0, (int)D, d_body);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_expand_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
+                            const uint32_t h_mask_key[8], uint64_t* d_ct, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if ((rc = seeded_args(ctx, B, D, d_body, d_id0, d_ct))) return rc;
+  if (!h_mask_key) return fail(ctx, FHE_E_ARG, "missing mask key");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  ChaKey Km;
+  for (int i = 0; i < 8; ++i) Km.w[i] = h_mask_key[i];
+  hipLaunchKernelGGL(k_expand_seeded, dim3((unsigned)(B * D)), dim3(256), 0, (hipStream_t)stream, Km, p.k * p.N,
+                     d_body, d_id0, (int)D, d_ct);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_linear_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
+                            const uint32_t h_mask_key[8], const int64_t* d_w, int64_t cst, uint64_t* d_out,
+                            void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if ((rc = seeded_args(ctx, B, D, d_body, d_id0, d_out))) return rc;
+  if (!h_mask_key || (B > 0 && !d_w)) return fail(ctx, FHE_E_ARG, "missing mask key or weights");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  ChaKey Km;
+  for (int i = 0; i < 8; ++i) Km.w[i] = h_mask_key[i];
+  hipLaunchKernelGGL(k_linear_seeded, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, Km, p.k * p.N, d_body,
+                     d_id0, (int)D, d_w, (u64)cst << (64 - p.msg_bits), d_out);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
 static int decrypt_mode(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, int64_t* d_out, int mode, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
@@ -1760,6 +1889,42 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
+}
+
+int fhe_compare_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
+                             const uint32_t h_mask_key[8], const int64_t* d_w, int64_t cst, int64_t T,
+                             int64_t* d_acc, int64_t* d_below, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if ((rc = seeded_args(ctx, B, D, d_body, d_id0, d_w))) return rc;
+  if (!h_mask_key || (B > 0 && (!d_acc || !d_below))) return fail(ctx, FHE_E_ARG, "bad seeded compare arguments");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
+  // workspace: ct_v (B big) | sign (B big) | small (B) | v (B)
+  rc = ensure_ws(ctx, 8 * (2 * (size_t)B * Wb + (size_t)B * Ws + (size_t)B));
+  if (rc) return rc;
+  u64* ctv = (u64*)ctx->ws;
+  u64* sgn = ctv + (size_t)B * Wb;
+  u64* small = sgn + (size_t)B * Wb;
+  int64_t* v = (int64_t*)(small + (size_t)B * Ws);
+  rc = fhe_linear_seeded_batch(ctx, d_body, d_id0, B, D, h_mask_key, d_w, cst - T, ctv, stream);
+  if (rc) return rc;
+  rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
+  if (rc) return rc;
+  rc = sign_extract(ctx, ctv, B, sgn, small, st);
+  if (rc) return rc;
+  rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+void fhe_key_from_seed(uint64_t seed, uint32_t h_key_out[8]) {
+  const ChaKey K = key_from_seed(seed);
+  for (int i = 0; i < 8; ++i) h_key_out[i] = K.w[i];
 }
 
 int fhe_quantize_pairs(fhe_ctx* ctx, const void* d_query, int32_t query_is_f64, const void* d_docs,

@@ -13,7 +13,11 @@ Changes for the GPU search path:
   * ``save_many`` writes a batch of documents and rewrites the index once;
   * ``corpus()`` returns ids and a stacked float32 [B, D] matrix in index
     order — the order that decides ties in search (:136-141) — cached until
-    the store changes, so a search uploads the corpus to HBM once.
+    the store changes, so a search uploads the corpus to HBM once;
+  * documents may carry a real ciphertext instead of the plaintext vector
+    (§8f-1): ``model_version == "fheicp-seeded-lwe-v1"`` marks an
+    ``encrypted_embedding`` that is a versioned seeded-LWE payload
+    (fheicp.corpus); ``encrypted_corpus()`` stacks those payloads.
 """
 from __future__ import annotations
 
@@ -31,6 +35,7 @@ import numpy as np
 logger = logging.getLogger(__name__)
 
 DEFAULT_DIMS = (128, 256)
+CIPHERTEXT_VERSION = "fheicp-seeded-lwe-v1"   # fheicp.corpus.PAYLOAD_VERSION
 
 
 @dataclass
@@ -56,6 +61,10 @@ class EncryptedDocument:
             raise TypeError("encrypted_embedding must be numpy array")
         if emb.ndim != 1:
             raise ValueError(f"Expected 1D embedding, got shape {emb.shape}")
+        if self.model_version == CIPHERTEXT_VERSION:
+            from fheicp.corpus import unpack_payload
+            unpack_payload(emb)  # raises ValueError on a malformed payload
+            return
         dims = type(self).allowed_dims
         if dims is not None and emb.shape[0] not in dims:
             raise ValueError(f"Expected embedding width in {tuple(dims)}, got {emb.shape}")
@@ -84,6 +93,7 @@ class EncryptedDocumentStore:
         self.index_file = self.storage_dir / "index.json"
         self.index: Dict[str, Dict[str, Any]] = self._load_index()
         self._corpus_cache = None
+        self._ct_cache = None
 
     # ------------------------------------------------------------ writes --
     def _write_doc(self, doc: EncryptedDocument) -> Path:
@@ -101,6 +111,7 @@ class EncryptedDocumentStore:
             "metadata": doc.metadata,
         }
         self._corpus_cache = None
+        self._ct_cache = None
         return self.storage_dir / name
 
     def save(self, doc: EncryptedDocument) -> str:
@@ -121,6 +132,7 @@ class EncryptedDocumentStore:
         if f.exists():
             f.unlink()
         self._corpus_cache = None
+        self._ct_cache = None
         self._save_index()
         return True
 
@@ -168,7 +180,10 @@ class EncryptedDocumentStore:
             if not ids:
                 self._corpus_cache = ([], np.zeros((0, 0), np.float32))
             else:
-                rows = [np.asarray(self.load(i).encrypted_embedding) for i in ids]
+                loaded = [self.load(i) for i in ids]
+                if any(d.model_version == CIPHERTEXT_VERSION for d in loaded):
+                    raise ValueError("store holds ciphertext documents: use encrypted_corpus()")
+                rows = [np.asarray(d.encrypted_embedding) for d in loaded]
                 widths = {r.shape[0] for r in rows}
                 if len(widths) != 1:
                     raise ValueError(f"store mixes embedding widths {sorted(widths)}")
@@ -178,6 +193,35 @@ class EncryptedDocumentStore:
                     raise ValueError(f"store mixes embedding dtypes {sorted(map(str, kinds))}")
                 self._corpus_cache = (ids, np.stack(rows))
         return self._corpus_cache
+
+    def encrypted_corpus(self):
+        """(doc_ids in index order, bodies uint64 [B, D], stream ids uint64 [B],
+        payload header {P0, mask_key, big, D}) of a store of ciphertext
+        documents. Cached like corpus()."""
+        if self._ct_cache is None:
+            from fheicp.corpus import unpack_payload
+            ids = list(self.index.keys())
+            if not ids:
+                self._ct_cache = ([], np.zeros((0, 0), np.uint64), np.zeros(0, np.uint64), None)
+            else:
+                pls = []
+                for i in ids:
+                    d = self.load(i)
+                    if d.model_version != CIPHERTEXT_VERSION:
+                        raise ValueError(f"document {i} is not a ciphertext document")
+                    pls.append(unpack_payload(d.encrypted_embedding))
+                head = {k: pls[0][k] for k in ("P0", "big", "D", "mask_key")}
+                for p in pls[1:]:
+                    if (p["P0"], p["big"], p["D"]) != (head["P0"], head["big"], head["D"]) or \
+                            not np.array_equal(p["mask_key"], head["mask_key"]):
+                        raise ValueError("store mixes ciphertext parameters or mask keys")
+                self._ct_cache = (ids, np.stack([p["body"] for p in pls]),
+                                  np.array([p["id0"] for p in pls], dtype=np.uint64), head)
+        return self._ct_cache
+
+    def holds_ciphertexts(self) -> bool:
+        ids = list(self.index.keys())
+        return bool(ids) and self.index[ids[0]].get("model_version") == CIPHERTEXT_VERSION
 
     # ------------------------------------------------------------- index --
     def _load_index(self) -> Dict[str, Dict[str, Any]]:

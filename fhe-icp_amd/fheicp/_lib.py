@@ -56,6 +56,11 @@ SIGNATURES = [
     ("fhe_sign_pbs_count", C.c_int, [_P]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
+    ("fhe_encrypt_seeded_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
+    ("fhe_expand_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
+    ("fhe_linear_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp, _vp]),
+    ("fhe_compare_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+    ("fhe_key_from_seed", None, [_u64, _vp]),
     ("fhe_quantize_pairs", C.c_int, [_CTXP, _vp, _i32, _vp, _i32, _i64, _i32, C.c_double, _i64, _i64, _i64, _vp, _vp]),
     ("fhe_dequantize", C.c_int, [_CTXP, _vp, _i64, C.c_double, _vp, _vp]),
     ("fhe_topk", C.c_int, [_CTXP, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),

@@ -13,6 +13,20 @@ from __future__ import annotations
 import numpy as np
 
 
+def training_embeddings(input_dim: int, n_samples: int = 1000, seed: int = 0):
+    """The (emb1, emb2) pairs behind training_pairs (same draws): calibration
+    data of the encrypted-corpus quantizer (fheicp.corpus)."""
+    rng = np.random.default_rng(seed)
+    emb1 = rng.standard_normal((n_samples, input_dim)).astype(np.float32)
+    emb1 = emb1 / np.linalg.norm(emb1, axis=1, keepdims=True)
+    emb2 = rng.standard_normal((n_samples, input_dim)).astype(np.float32)
+    emb2 = emb2 / np.linalg.norm(emb2, axis=1, keepdims=True)
+    mask = rng.random(n_samples) > 0.5
+    emb2[mask] = emb1[mask] + 0.2 * rng.standard_normal((int(mask.sum()), input_dim))
+    emb2 = emb2 / np.linalg.norm(emb2, axis=1, keepdims=True)
+    return emb1, emb2
+
+
 def training_pairs(input_dim: int, n_samples: int = 1000, seed: int = 0, similarity_type: str = "cosine"):
     rng = np.random.default_rng(seed)
     emb1 = rng.standard_normal((n_samples, input_dim)).astype(np.float32)

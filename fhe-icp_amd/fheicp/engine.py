@@ -188,6 +188,58 @@ class Engine:
                                             _stream(self.device)))
         return acc, below
 
+    # ------------------------------------------- seeded (stored) corpus --
+    @staticmethod
+    def key_from_seed(seed: int) -> np.ndarray:
+        out = np.zeros(8, np.uint32)
+        _lib.lib().fhe_key_from_seed(C.c_uint64(seed), C.c_void_p(out.ctypes.data))
+        return out
+
+    @staticmethod
+    def _key(k) -> C.Array:
+        k = np.ascontiguousarray(k, dtype=np.uint32).reshape(8)
+        return (C.c_uint32 * 8)(*[int(x) for x in k])
+
+    def quantize(self, x: torch.Tensor, scale: float, zero_point: int, qmin: int, qmax: int) -> torch.Tensor:
+        """clip(rint(x / scale + zp), qmin, qmax) of a device f32/f64 [B, D] (fhe_quantize_pairs)."""
+        B, D = x.shape
+        q = torch.empty((B, D), dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_quantize_pairs(self._ctx, None, 0, _ptr(x), 1 if x.dtype == torch.float64 else 0, B, D,
+                                             C.c_double(scale), int(zero_point), int(qmin), int(qmax), _ptr(q),
+                                             _stream(self.device)))
+        return q
+
+    def encrypt_seeded(self, msg: torch.Tensor, mask_key, noise_key, id0: torch.Tensor) -> torch.Tensor:
+        B, D = msg.shape
+        body = torch.empty((B, D), dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_encrypt_seeded_batch(self._ctx, _ptr(msg), B, D, self._key(mask_key),
+                                                   self._key(noise_key), _ptr(id0), _ptr(body), _stream(self.device)))
+        return body
+
+    def expand_seeded(self, body: torch.Tensor, id0: torch.Tensor, B: int, D: int, mask_key) -> torch.Tensor:
+        ct = self.empty_big(B * D)
+        self._chk(self._L.fhe_expand_seeded_batch(self._ctx, _ptr(body), _ptr(id0), B, D, self._key(mask_key),
+                                                  _ptr(ct), _stream(self.device)))
+        return ct
+
+    def linear_seeded(self, body: torch.Tensor, id0: torch.Tensor, mask_key, w, cst: int) -> torch.Tensor:
+        B, D = body.shape
+        wd = self.to_dev(w)
+        out = self.empty_big(B)
+        self._chk(self._L.fhe_linear_seeded_batch(self._ctx, _ptr(body), _ptr(id0), B, D, self._key(mask_key),
+                                                  _ptr(wd), int(cst), _ptr(out), _stream(self.device)))
+        return out
+
+    def compare_seeded(self, body: torch.Tensor, id0: torch.Tensor, mask_key, w: torch.Tensor, cst: int, T: int):
+        """fhe_compare_seeded_batch: (acc int64[B], below int64[B])."""
+        B, D = body.shape
+        acc = torch.empty(B, dtype=torch.int64, device=self.device)
+        below = torch.empty(B, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_compare_seeded_batch(self._ctx, _ptr(body), _ptr(id0), B, D, self._key(mask_key),
+                                                   _ptr(w), int(cst), int(T), _ptr(acc), _ptr(below),
+                                                   _stream(self.device)))
+        return acc, below
+
     def topk(self, acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx: int = 0):
         oa = torch.empty(k, dtype=torch.int64, device=self.device)
         oi = torch.empty(k, dtype=torch.int64, device=self.device)

@@ -52,3 +52,42 @@ def load_model(path: str):
             raise ValueError(f"{path}: format version {meta['version']} is newer than supported {VERSION}")
         keys = {k: z[k].copy() for k in KEY_NAMES} if all(k in z.files for k in KEY_NAMES) else None
     return QuantParams.from_dict(meta["quant"]), SchemeParams(**meta["scheme"]), keys
+
+
+CORPUS_FORMAT = "fheicp-corpus"
+CORPUS_VERSION = 1
+
+
+def save_corpus(path: str, corpus) -> None:
+    """Persist an EncryptedCorpus (fheicp.corpus): the model's quantisation,
+    the corpus quantizer, the scheme, the PUBLIC mask key and the secret
+    keys. Stored documents (seeded LWEs) are searchable again only with these
+    keys; the session-local noise key is not stored (it is needed only to
+    encrypt, and a fresh one is drawn per session)."""
+    meta = {"format": CORPUS_FORMAT, "version": CORPUS_VERSION, "quant": corpus.cq.model.to_dict(),
+            "corpus": corpus.cq.to_dict(), "P0": int(corpus.P0), "scheme": corpus.scheme.as_dict(),
+            "mask_key": [int(x) for x in corpus.mask_key]}
+    arrays = {"meta": np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)}
+    keys = corpus.engine.export_keys()
+    for k in KEY_NAMES:
+        arrays[k] = np.ascontiguousarray(keys[k], dtype=np.uint64)
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, **arrays)
+    os.replace(tmp, path)
+
+
+def load_corpus(path: str, device: int = 0):
+    """-> a compiled EncryptedCorpus with the stored keys and mask key."""
+    from .corpus import CorpusQuant, EncryptedCorpus
+    with np.load(path, allow_pickle=False) as z:
+        meta = json.loads(bytes(z["meta"]).decode())
+        if meta.get("format") != CORPUS_FORMAT:
+            raise ValueError(f"{path}: not an {CORPUS_FORMAT} file")
+        if int(meta.get("version", 0)) > CORPUS_VERSION:
+            raise ValueError(f"{path}: format version {meta['version']} is newer than supported {CORPUS_VERSION}")
+        keys = {k: z[k].copy() for k in KEY_NAMES}
+    cq = CorpusQuant(QuantParams.from_dict(meta["quant"]), int(meta["corpus"]["n_e"]), float(meta["corpus"]["s_e"]))
+    c = EncryptedCorpus(cq, SchemeParams(**meta["scheme"]))
+    if c.P0 != int(meta["P0"]):
+        raise ValueError(f"{path}: stored P0 {meta['P0']} does not match the quantizer's {c.P0}")
+    return c.compile(device=device, keys=keys, mask_key=np.asarray(meta["mask_key"], dtype=np.uint32))

@@ -159,6 +159,38 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
 int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                       int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream);
 
+/* ---- seeded (compressed) ciphertexts: the encrypted document corpus -------
+ * Persisted documents (EncryptedDocument at
+ * encrypted_storage.py:19-51, whose `encrypted_embedding` is a plaintext
+ * vector in the reference, batch_operations.py:175-178) are stored as
+ * seeded LWEs: only the body word per feature. The mask of feature j of
+ * document b is ChaCha20 stream (TAG_ENC_MASK, id0[b] + j) under the PUBLIC
+ * 256-bit mask key; the noise comes from the SECRET noise key. A corpus in
+ * HBM is then B x D body words plus B ids instead of B x D x (kN + 1) words;
+ * the masks are regenerated inside the kernels that consume them.
+ * d_msg / d_body: B x D (row-major), d_id0: B u64 (stream ids must not repeat
+ * under one mask key). */
+int fhe_encrypt_seeded_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t B, int32_t D, const uint32_t h_mask_key[8],
+                             const uint32_t h_noise_key[8], const uint64_t* d_id0, uint64_t* d_body, void* stream);
+/* full ciphertexts (B*D x (kN+1)) of a seeded corpus; needs no secret key */
+int fhe_expand_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
+                            const uint32_t h_mask_key[8], uint64_t* d_ct, void* stream);
+/* fhe_linear_batch on a seeded corpus (masks regenerated in registers):
+ * out[b] = sum_j d_w[j] * ct(b, j) + trivial(cst * Delta); B x (kN+1). */
+int fhe_linear_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
+                            const uint32_t h_mask_key[8], const int64_t* d_w, int64_t cst, uint64_t* d_out,
+                            void* stream);
+/* fhe_compare_batch over a stored encrypted corpus: linear (seeded) with d_w
+ * and cst - T -> decrypt the leveled accumulator -> sign extraction ->
+ * decrypt the threshold bit. The documents were encrypted at some P0 >= the
+ * context's msg_bits P; the caller folds 2^(P0 - P) into d_w. */
+int fhe_compare_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
+                             const uint32_t h_mask_key[8], const int64_t* d_w, int64_t cst, int64_t T,
+                             int64_t* d_acc, int64_t* d_below, void* stream);
+/* The 64-bit-seed -> 256-bit ChaCha key expansion used by fhe_keygen and
+ * fhe_encrypt_batch (splitmix64). Host only. */
+void fhe_key_from_seed(uint64_t seed, uint32_t h_key_out[8]);
+
 /* ---- clear pre/post-processing on the device ----------------------------
  * Pair features and Concrete-ML's input quantizer in one pass:
  * X[b, j] = query[j] * docs[b, j] in numpy's promoted dtype (the query may be

@@ -273,3 +273,59 @@ def message_bits(params: QuantizedLinearParams) -> int:
     lo, hi = acc_bounds(params)
     rng = hi - lo
     return int(math.ceil(math.log2(rng + 2))) + 1
+
+
+# --------------------------------------------------------------------------
+# Encrypted-corpus mode. The reference has
+# no such mode — its stored "encrypted_embedding" is the plaintext vector
+# (batch_operations.py:175-178) — so this is a restatement of this build's
+# own spec: documents and the query are quantized separately with one
+# symmetric signed n_e-bit quantizer (Concrete-ML is_symmetric=True
+# calibration), the product's quantisation becomes the product of the
+# quantized values, and the bias moves to the scale (s_e * s_e) * s_w.
+# --------------------------------------------------------------------------
+def corpus_scale(embeddings, n_e: int) -> float:
+    q = UniformQuantizer(n_e, is_signed=True, is_symmetric=True).calibrate(np.asarray(embeddings).reshape(-1))
+    return q.scale
+
+
+def corpus_quant(s_e: float, n_e: int, v) -> np.ndarray:
+    return UniformQuantizer(n_e, True, True, s_e, 0).quant(v)
+
+
+def corpus_out_scale(params: QuantizedLinearParams, s_e: float) -> float:
+    return float((np.float64(s_e) * np.float64(s_e)) * np.float64(params.s_w))
+
+
+def corpus_qb(params: QuantizedLinearParams, s_e: float) -> int:
+    return int(np.rint(np.float64(params.intercept) / np.float64(corpus_out_scale(params, s_e))))
+
+
+def corpus_accumulate(params: QuantizedLinearParams, s_e: float, n_e: int, query, docs) -> np.ndarray:
+    """acc[b] = sum_j q_w[j] * qq_j * dq[b, j] + q_b' in int64."""
+    qq = corpus_quant(s_e, n_e, query)
+    dq = corpus_quant(s_e, n_e, np.atleast_2d(docs))
+    return dq @ (params.q_w * qq) + np.int64(corpus_qb(params, s_e))
+
+
+def corpus_bounds(params: QuantizedLinearParams, s_e: float, n_e: int, query):
+    W = params.q_w * corpus_quant(s_e, n_e, query)
+    qmin, qmax = -(2 ** (n_e - 1)), 2 ** (n_e - 1) - 1
+    c = corpus_qb(params, s_e)
+    return int(np.minimum(W * qmin, W * qmax).sum()) + c, int(np.maximum(W * qmin, W * qmax).sum()) + c
+
+
+def corpus_worst_bits(params: QuantizedLinearParams, s_e: float, n_e: int) -> int:
+    bound = int(np.abs(params.q_w).sum()) * 4 ** (n_e - 1) + abs(corpus_qb(params, s_e))
+    return int(math.ceil(math.log2(2 * bound + 2))) + 1
+
+
+def corpus_search(params: QuantizedLinearParams, s_e: float, n_e: int, query, docs, top_k: int,
+                  min_similarity: float):
+    """batch_operations.py:268-284 semantics (float >=, stable sort desc,
+    [:top_k]) on the encrypted-corpus scores: list of (index, score)."""
+    s = np.float64(corpus_out_scale(params, s_e))
+    scores = s * corpus_accumulate(params, s_e, n_e, query, docs).astype(np.float64)
+    sims = [(i, float(scores[i])) for i in range(len(scores)) if scores[i] >= min_similarity]
+    sims.sort(key=lambda x: x[1], reverse=True)
+    return sims[:top_k]

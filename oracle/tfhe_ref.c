@@ -264,6 +264,49 @@ void ref_encrypt_ints(const ref_params* P, const uint64_t* s_big, const int64_t*
   free(m);
 }
 
+/* Seeded encryption of a document corpus: feature j of
+ * document b has stream id id0[b] + j; its mask is the TAG_ENC_MASK stream
+ * of the public key `mkey`, its noise the TAG_ENC_NOISE stream of the
+ * secret key `nkey`. Only the bodies are produced (B x D). */
+void ref_encrypt_seeded(const ref_params* P, const uint64_t* s_big, const int64_t* v, int64_t B, int32_t D,
+                        const uint32_t mkey[8], const uint32_t nkey[8], const uint64_t* id0, uint64_t* body) {
+  ref_key Km, Kn;
+  memcpy(Km.key, mkey, 32);
+  memcpy(Kn.key, nkey, 32);
+  const int dim = P->k * P->N;
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < B * D; ++c) {
+    const uint64_t id = id0[c / D] + (uint64_t)(c % D);
+    ref_stream sm, sn;
+    stream_init(&sm, &Km, TAG_ENC_MASK, id);
+    stream_init(&sn, &Kn, TAG_ENC_NOISE, id);
+    uint64_t b = 0;
+    for (int t = 0; t < dim; ++t)
+      if (s_big[t]) b += stream_word(&sm, (uint64_t)t);
+    b += (uint64_t)tuniform(stream_word(&sn, 0), P->glwe_noise_bits);
+    body[c] = b + (((uint64_t)v[c]) << (64 - P->msg_bits));
+  }
+}
+/* full ciphertexts (B*D x (kN+1)) of a seeded corpus */
+void ref_expand_seeded(const ref_params* P, const uint64_t* body, const uint64_t* id0, int64_t B, int32_t D,
+                       const uint32_t mkey[8], uint64_t* ct) {
+  ref_key Km;
+  memcpy(Km.key, mkey, 32);
+  const int dim = P->k * P->N;
+  for (int64_t c = 0; c < B * D; ++c) {
+    ref_stream sm;
+    stream_init(&sm, &Km, TAG_ENC_MASK, id0[c / D] + (uint64_t)(c % D));
+    uint64_t* o = ct + (size_t)c * (dim + 1);
+    for (int t = 0; t < dim; ++t) o[t] = stream_word(&sm, (uint64_t)t);
+    o[dim] = body[c];
+  }
+}
+void ref_key_from_seed(uint64_t seed, uint32_t out[8]) {
+  ref_key K;
+  key_from_seed(seed, &K);
+  memcpy(out, K.key, 32);
+}
+
 static uint64_t lwe_phase(const uint64_t* ct, const uint64_t* s, int dim) {
   uint64_t acc = ct[dim];
   for (int t = 0; t < dim; ++t)

@@ -63,6 +63,9 @@ def lib():
         L.ref_decompose.argtypes = [C.c_uint64, C.c_int, C.c_int, i64p]
         L.ref_tuniform.argtypes = [C.c_uint64, C.c_int]; L.ref_tuniform.restype = C.c_int64
         L.ref_chacha20_block.argtypes = [u32p, C.c_uint32, u32p, u32p]
+        L.ref_encrypt_seeded.argtypes = [P, u64p, i64p, C.c_int64, C.c_int32, u32p, u32p, u64p, u64p]
+        L.ref_expand_seeded.argtypes = [P, u64p, u64p, C.c_int64, C.c_int32, u32p, u64p]
+        L.ref_key_from_seed.argtypes = [C.c_uint64, u32p]
         _lib = L
     return _lib
 
@@ -111,6 +114,27 @@ class RefTFHE:
         msg = np.ascontiguousarray(msg, dtype=np.uint64).reshape(-1)
         ct = np.zeros((msg.size, self.big + 1), np.uint64)
         lib().ref_encrypt_raw(C.byref(self.P), u64(self.s_big), u64(msg), msg.size, seed, id0, u64(ct))
+        return ct
+
+    def encrypt_seeded(self, v, mask_key, noise_key, id0) -> np.ndarray:
+        """Seeded corpus encryption (bodies only), v: B x D ints, id0: B stream ids."""
+        v = np.ascontiguousarray(v, dtype=np.int64)
+        B, D = v.shape
+        ids = np.ascontiguousarray(id0, dtype=np.uint64)
+        mk = np.ascontiguousarray(mask_key, dtype=np.uint32)
+        nk = np.ascontiguousarray(noise_key, dtype=np.uint32)
+        body = np.zeros((B, D), np.uint64)
+        lib().ref_encrypt_seeded(C.byref(self.P), u64(self.s_big), i64(v), B, D, _p(mk, C.c_uint32),
+                                 _p(nk, C.c_uint32), u64(ids), u64(body))
+        return body
+
+    def expand_seeded(self, body, id0, mask_key) -> np.ndarray:
+        body = np.ascontiguousarray(body, dtype=np.uint64)
+        B, D = body.shape
+        ids = np.ascontiguousarray(id0, dtype=np.uint64)
+        mk = np.ascontiguousarray(mask_key, dtype=np.uint32)
+        ct = np.zeros((B * D, self.big + 1), np.uint64)
+        lib().ref_expand_seeded(C.byref(self.P), u64(body), u64(ids), B, D, _p(mk, C.c_uint32), u64(ct))
         return ct
 
     def phase(self, ct: np.ndarray, small: bool = False) -> np.ndarray:
@@ -212,6 +236,12 @@ def chacha20_block(key_words, counter: int, nonce_words) -> np.ndarray:
     n = np.ascontiguousarray(nonce_words, dtype=np.uint32)
     out = np.zeros(16, np.uint32)
     lib().ref_chacha20_block(_p(k, C.c_uint32), counter, _p(n, C.c_uint32), _p(out, C.c_uint32))
+    return out
+
+
+def key_from_seed(seed: int) -> np.ndarray:
+    out = np.zeros(8, np.uint32)
+    lib().ref_key_from_seed(C.c_uint64(seed), _p(out, C.c_uint32))
     return out
 
 
