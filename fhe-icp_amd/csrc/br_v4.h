@@ -25,12 +25,15 @@ namespace v4 {
 using u64 = uint64_t;
 
 constexpr int M = 512, N = 1024, S = 8, K = 2;
-constexpr int G = 2;             // ciphertexts per workgroup
 constexpr int WPC = K + 1;       // waves per ciphertext
-constexpr int NT = 64 * G * WPC; // 384 threads
-constexpr int NTW = 15;          // per-lane twiddle entries: 8 for pass A (twist merged), 7 for pass B
+// ciphertexts per workgroup: G2 = 2 (384 threads, 2 workgroups per CU) or 1
+// (192 threads, 4 workgroups per CU: barriers join only one ciphertext's waves)
+constexpr int nthreads(int G) { return 64 * G * WPC; }
+constexpr int NTA = 8 * 64;      // pass A twiddles: 8 per lane (twist merged)
+constexpr int NTB = 7 * 8;       // pass B twiddles: 7 per value of the 3 index bits below the pass
+constexpr int NTW = NTA + NTB;   // LDS twiddle table entries (9 KB)
 constexpr int NMAX = 1023;       // max small-LWE dimension (LDS budget: 2 workgroups per CU)
-constexpr int SCR = 528;         // relayout scratch elements per wave (positions < 527)
+constexpr int SCR = 576;         // relayout scratch elements per wave (positions < 573)
 
 // Transform = three radix-8 passes over index bits (8,7,6), (5,4,3), (2,1,0).
 // A pass runs a constant DFT-8 network on its 3 slot bits (internal
@@ -44,8 +47,8 @@ struct Lay {
   int p[9];
 };
 constexpr Lay LAYS[3] = {{{6, 7, 8, 0, 1, 2, 3, 4, 5}},   // LA: natural, j = lane + 64 u
-                         {{3, 4, 5, 2, 8, 1, 0, 7, 6}},   // LB
-                         {{0, 1, 2, 5, 6, 7, 3, 4, 8}}};  // LC: transform output
+                         {{3, 4, 5, 0, 1, 2, 6, 7, 8}},   // LB: LA with slot bits k <-> lane bits 3 + k
+                         {{0, 1, 2, 4, 5, 8, 3, 6, 7}}};  // LC: transform output
 enum { LA = 0, LB = 1, LC = 2 };
 
 __host__ __device__ constexpr int jof(int li, int lane, int u) {
@@ -60,8 +63,11 @@ __host__ __device__ constexpr int jof(int li, int lane, int u) {
 // one base register plus immediate offsets). The offsets were searched so
 // that the 8-lane ds_write_b128 groups of the source layout and the 16-lane
 // ds_read_b128 groups of the target layout hit distinct bank quads.
-enum { R1F = 0, R1I = 1, R2F = 2, R2I = 3 };  // LA->LB, LB->LA, LB->LC, LC->LB
-constexpr int RC[4][5] = {{0, 0, 0, 0, 8}, {0, 0, 0, 0, 1}, {0, 1, 2, 4, 7}, {0, 1, 2, 4, 8}};
+// LA <-> LB is not an LDS relayout any more: it exchanges the slot bits with
+// lane bits 3..5 in registers (swap_lb below); only LB <-> LC goes through
+// LDS (offsets from tools/search_relayout.py --lb 0,1,2,6,7,8).
+enum { R2F = 0, R2I = 1 };  // LB->LC, LC->LB
+constexpr int RC[2][5] = {{1, 2, 4, 7, 16}, {2, 4, 8, 16, 31}};
 __host__ __device__ constexpr int rpos(int r, int j) {
   int p = j;
   for (int k = 0; k < 5; ++k) p += RC[r][k] * ((j >> (4 + k)) & 1);
@@ -70,23 +76,66 @@ __host__ __device__ constexpr int rpos(int r, int j) {
 
 __host__ __device__ constexpr int bitrev3(int u) { return ((u & 1) << 2) | (u & 2) | ((u >> 2) & 1); }
 
-// Per-lane twiddles, twl[e][lane], computed on the host in long double
-// (v4_twiddles) and copied to LDS per workgroup:
-//   e = m (0..7):      pass A, w^lane * exp(2 pi i lane m / 512) — the lane
-//                      part w^lane of the fold twist w^(lane + 64 u)
-//                      (w = exp(i pi / N)) commutes with pass A's DFT-8 and
-//                      merges into its lane twiddles;
-//   e = 7 + m (1..7):  pass B, exp(2 pi i L m / 64), L = index bits 0..2.
+// Twiddles, computed on the host in long double (fhe_ctx_create) and copied
+// to LDS per workgroup:
+//   twl[m * 64 + lane] (m = 0..7): pass A, w^lane * exp(2 pi i lane m / 512)
+//        — the lane part w^lane of the fold twist w^(lane + 64 u)
+//        (w = exp(i pi / N)) commutes with pass A's DFT-8 and merges into
+//        its lane twiddles;
+//   twl[NTA + (m - 1) * 8 + L] (m = 1..7): pass B, exp(2 pi i L m / 64),
+//        L = index bits 0..2 of the lane in layout LB (lanes sharing L read
+//        one address: an LDS broadcast).
 // The slot part w^(64 u) = exp(i pi u / 16) is a compile-time constant (fold8).
-__host__ __device__ inline int v4_tw_pass(int e) { return e < 8 ? 0 : 1; }
+__host__ __device__ constexpr int lb_low3(int lane) { return jof(1, lane, 0) & 7; }
 __device__ __forceinline__ void fill_tables(c64* twl, const c64* __restrict__ tw4, int tid, int nthr) {
-  for (int x = tid; x < NTW * 64; x += nthr) twl[x] = tw4[x];
+  for (int x = tid; x < NTW; x += nthr) twl[x] = tw4[x];
 }
 
 // Workgroup barrier for LDS hand-offs only: retire this wave's LDS ops, then
 // s_barrier. Outstanding global loads stay in flight across it (the compiler
 // sees neither a fence nor a barrier it would drain them for).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Per-ciphertext hand-offs without s_barrier (FL kernels): the three waves of
+// a ciphertext count their F writes (W) and their reads of the others' F (R)
+// in two LDS words. One wave's DS operations are performed in order, so a
+// count added after a wave's F writes (or after its reads) is observed only
+// once those have been performed; the compiler is kept from moving LDS
+// accesses across the add and the poll by "memory" clobbers. Outstanding
+// global loads are not waited for. Ciphertexts of a workgroup never wait for
+// each other, unlike s_barrier.
+// Both are inline asm so that no divergent branch or loop appears in the
+// compiler's CFG (a divergent `if (lane == 0)` there made the allocator
+// spill the prefetched BSK rows).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ void ct_signal(uint32_t* f) {
+  uint64_t saved;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %1, %2\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(saved)
+      : "v"(lds_addr(f)), "v"(1u)
+      : "memory");
+}
+__device__ __forceinline__ void ct_wait(const uint32_t* f, uint32_t target) {
+  uint32_t tv;
+  uint32_t ts;
+  asm volatile(
+      "1:\n\t"
+      "ds_read_b32 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %1, %0\n\t"
+      "s_cmp_lt_u32 %1, %3\n\t"
+      "s_cbranch_scc0 2f\n\t"
+      "s_sleep 1\n\t"
+      "s_branch 1b\n"
+      "2:"
+      : "=&v"(tv), "=&s"(ts)
+      : "v"(lds_addr(f)), "s"(target)
+      : "memory", "scc");
+}
 
 // ---- register-level pieces ---------------------------------------------
 constexpr double RH = 0.70710678118654752440;  // sqrt(2)/2
@@ -151,13 +200,14 @@ __device__ __forceinline__ void idft8(c64 (&v)[S]) {
 // DBG bit 0 takes them from wf
 template <int PS, bool INV, int DBG = 0>
 __device__ __forceinline__ void lane_tw(c64 (&v)[S], const c64* twl, int lane, c64 wf) {
-  constexpr int M0 = PS == 0 ? 0 : 1, E0 = PS == 0 ? 0 : 7;
+  constexpr int M0 = PS == 0 ? 0 : 1;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int m0 = h ? 4 : M0, m1 = h ? 7 : 3;
     c64 T[4];
 #pragma unroll
-    for (int m = m0; m <= m1; ++m) T[m - m0] = (DBG & 1) ? wf : twl[(E0 + m) * 64 + lane];
+    for (int m = m0; m <= m1; ++m)
+      T[m - m0] = (DBG & 1) ? wf : PS == 0 ? twl[m * 64 + lane] : twl[NTA + (m - 1) * 8 + lb_low3(lane)];
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int m = bitrev3(u);
@@ -194,6 +244,51 @@ __device__ __forceinline__ void relayout(c64 (&v)[S], c64* scr, int lane) {
   for (int u = 0; u < S; ++u) v[u] = scr[rpos(R, jof(LT, lane, u))];
 }
 
+// LA <-> LB in registers (self-inverse): slot bit 2 <-> lane bit 5 by
+// v_permlane32_swap, slot bit 1 <-> lane bit 4 by v_permlane16_swap (both
+// exchange half-rows between two registers), slot bit 0 <-> lane bit 3 by
+// two DPP row shifts of 8 lanes whose bank masks keep the half-rows that stay.
+__device__ __forceinline__ uint32_t dpp_shr8_hi(uint32_t old, uint32_t src) {  // banks 2,3 <- src[lane - 8]
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, 0x118, 0xF, 0xC, false);
+}
+__device__ __forceinline__ uint32_t dpp_shl8_lo(uint32_t old, uint32_t src) {  // banks 0,1 <- src[lane + 8]
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, 0x108, 0xF, 0x3, false);
+}
+template <int KIND>  // 0: permlane32 (slot bit 2), 1: permlane16 (slot bit 1), 2: dpp (slot bit 0)
+__device__ __forceinline__ void swap_pair(double& x, double& y) {
+  const uint64_t xb = __builtin_bit_cast(uint64_t, x), yb = __builtin_bit_cast(uint64_t, y);
+  uint32_t x0 = (uint32_t)xb, x1 = (uint32_t)(xb >> 32), y0 = (uint32_t)yb, y1 = (uint32_t)(yb >> 32);
+  if constexpr (KIND == 0) {
+    auto a = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+    auto b = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+    x0 = a[0], y0 = a[1], x1 = b[0], y1 = b[1];
+  } else if constexpr (KIND == 1) {
+    auto a = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+    auto b = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+    x0 = a[0], y0 = a[1], x1 = b[0], y1 = b[1];
+  } else {
+    const uint32_t nx0 = dpp_shr8_hi(x0, y0), nx1 = dpp_shr8_hi(x1, y1);
+    const uint32_t ny0 = dpp_shl8_lo(y0, x0), ny1 = dpp_shl8_lo(y1, x1);
+    x0 = nx0, x1 = nx1, y0 = ny0, y1 = ny1;
+  }
+  x = __builtin_bit_cast(double, (uint64_t)x0 | ((uint64_t)x1 << 32));
+  y = __builtin_bit_cast(double, (uint64_t)y0 | ((uint64_t)y1 << 32));
+}
+template <int KIND, int STRIDE>
+__device__ __forceinline__ void swap_bit(c64 (&v)[S]) {
+#pragma unroll
+  for (int u = 0; u < S; ++u) {
+    if (u & STRIDE) continue;
+    swap_pair<KIND>(v[u].x, v[u + STRIDE].x);
+    swap_pair<KIND>(v[u].y, v[u + STRIDE].y);
+  }
+}
+__device__ __forceinline__ void swap_lb(c64 (&v)[S]) {
+  swap_bit<0, 4>(v);
+  swap_bit<1, 2>(v);
+  swap_bit<2, 1>(v);
+}
+
 // folded coefficient pairs (a_t + i a_{t+M}), natural order (LA) -> LC;
 // includes the negacyclic twist w^t
 template <int DBG = 0>
@@ -201,7 +296,7 @@ __device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, i
   fold8<false>(v);
   dft8(v);
   lane_tw<0, false, DBG>(v, twl, lane, wf);
-  relayout<R1F, LA, LB, DBG>(v, scr, lane);
+  if constexpr ((DBG & 8) == 0) swap_lb(v);
   dft8(v);
   lane_tw<1, false, DBG>(v, twl, lane, wf);
   relayout<R2F, LB, LC, DBG>(v, scr, lane);
@@ -214,7 +309,7 @@ __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, i
   relayout<R2I, LC, LB, DBG>(v, scr, lane);
   lane_tw<1, true, DBG>(v, twl, lane, wf);
   idft8(v);
-  relayout<R1I, LB, LA, DBG>(v, scr, lane);
+  if constexpr ((DBG & 8) == 0) swap_lb(v);
   lane_tw<0, true, DBG>(v, twl, lane, wf);
   idft8(v);
   fold8<true>(v);

@@ -843,7 +843,7 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
 __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bsk, int npoly,
                                                       const c64* __restrict__ tw4, c64* __restrict__ out) {
   using namespace v4;
-  __shared__ c64 twl[NTW * 64];
+  __shared__ c64 twl[NTW];
   __shared__ c64 scr[SCR];
   const int lane = threadIdx.x;
   fill_tables(twl, tw4, lane, 64);
@@ -893,6 +893,8 @@ __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int bet
 // Phase timestamps (DBG bit 7): wave 0 of workgroup 0 records s_memtime at
 // the phase boundaries of steps 100..103 (tools/prof_br.py --stamps).
 __device__ unsigned long long g_v4_stamps[4][16];
+// ... and every workgroup's {s_memrealtime at start, at end, HW_ID} (first 2048)
+__device__ unsigned long long g_v4_span[2048][3];
 #define V4_STAMP(k)                                                                        \
   do {                                                                                     \
     if constexpr ((DBG & 128) != 0) stamp_[k] = __builtin_amdgcn_s_memtime();              \
@@ -902,8 +904,8 @@ __device__ unsigned long long g_v4_stamps[4][16];
 // 1 twiddles from a register, 2 no BSK loads, 4 no barriers, 8 no FFT
 // relayout, 16 no LDS rotation, 32 no LDS reads of the other components,
 // 128 phase timestamps (results correct).
-template <int L, bool A32, int DBG = 0>
-__global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
+template <int L, bool A32, int DBG = 0, int G = 2, bool FL = false>
+__global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
                                                               const c64* __restrict__ tw4, BrTv tv, int mode,
                                                               u64* __restrict__ out, u64* __restrict__ ct_v,
@@ -911,9 +913,11 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
   using namespace v4;
   using AT = Acc<A32>;
   using T = typename AT::T;
+  constexpr int NT = nthreads(G);
   __shared__ c64 xbuf[G * WPC * SCR];  // one 8.5 KB slot per wave
-  __shared__ c64 twl[NTW * 64];
+  __shared__ c64 twl[NTW];
   __shared__ uint16_t atab[G][NMAX + 1];
+  __shared__ uint32_t ctflag[G][2];  // FL: per-ciphertext W / R hand-off counts
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = w / WPC, comp = w - g * WPC;
@@ -922,13 +926,22 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
   const c64* ctslots = xbuf + g * WPC * SCR;
   T* sa = reinterpret_cast<T*>(slot);
 
+  if constexpr ((DBG & 128) != 0)
+    if (tid == 0 && blockIdx.x < 2048) {
+      g_v4_span[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+      g_v4_span[blockIdx.x][2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
   fill_tables(twl, tw4, tid, NT);
   for (int x = tid; x < G * (n + 1); x += NT) {
     const int gg = x / (n + 1), ii = x - gg * (n + 1);
     const int64_t cc = (int64_t)blockIdx.x * G + gg;
     atab[gg][ii] = cc < count ? (uint16_t)modswitch_2n(small[(size_t)cc * (n + 1) + ii], 11) : (uint16_t)0;
   }
+  if (tid < 2 * G) ctflag[tid >> 1][tid & 1] = 0;
   __syncthreads();
+  uint32_t* fW = &ctflag[g][0];
+  uint32_t* fR = &ctflag[g][1];
+  uint32_t phase = 0;  // FL: hand-offs completed by this ciphertext
 
   T acc[2 * S];
   {
@@ -944,8 +957,9 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
   const c64 wf = {0.5 + (double)beta * 1e-3, (double)L * 1e-3};  // DBG stand-in value
   for (int i = 0; i < n; ++i) {
     const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)atab[g][i]);
-    [[maybe_unused]] unsigned long long stamp_[14];
+    [[maybe_unused]] unsigned long long stamp_[16];
     V4_STAMP(0);
+    if constexpr ((DBG & 128) != 0) stamp_[14] = __builtin_amdgcn_s_memrealtime();
     // X^a ACC - ACC through the wave's slot, then the gadget digits
     if constexpr ((DBG & 16) == 0) {
 #pragma unroll
@@ -993,6 +1007,10 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
 #pragma unroll
         for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gp[u * 64 + lane];
       }
+      // FL: the others must have read this slot's previous F before the
+      // transform's relayouts overwrite it
+      if constexpr (FL && (DBG & 4) == 0)
+        if (lv > 0) ct_wait(fR, 3 * phase);
       forward<DBG>(v, twl, slot, lane, wf);
       V4_STAMP(2 + 5 * lv);
 #pragma unroll
@@ -1010,7 +1028,14 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
         for (int u = 0; u < S; ++u) kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
       }
       V4_STAMP(3 + 5 * lv);
-      if constexpr ((DBG & 4) == 0) lds_barrier();
+      if constexpr ((DBG & 4) == 0) {
+        if constexpr (FL) {
+          ct_signal(fW);
+          ct_wait(fW, 3 * (phase + 1));
+        } else {
+          lds_barrier();
+        }
+      }
       V4_STAMP(4 + 5 * lv);
 #pragma unroll
       for (int ci = 0; ci < K; ++ci) {
@@ -1026,9 +1051,17 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
         }
       }
       V4_STAMP(5 + 5 * lv);
-      if constexpr ((DBG & 4) == 0) lds_barrier();
+      if constexpr ((DBG & 4) == 0) {
+        if constexpr (FL) {
+          ct_signal(fR);
+          ++phase;
+        } else {
+          lds_barrier();
+        }
+      }
       V4_STAMP(6 + 5 * lv);
     }
+    if constexpr (FL && (DBG & 4) == 0) ct_wait(fR, 3 * phase);
     inverse<DBG>(mac, twl, slot, lane, wf);
     V4_STAMP(12);
 #pragma unroll
@@ -1037,15 +1070,18 @@ __global__ void __launch_bounds__(v4::NT, A32 ? 3 : 2) k_blind_rotate_v4(const u
       acc[u + S] += AT::from_f64(mac[u].y);
     }
     V4_STAMP(13);
+    if constexpr ((DBG & 128) != 0) stamp_[15] = __builtin_amdgcn_s_memrealtime();
     if constexpr ((DBG & 128) != 0)
-      if (blockIdx.x == 0 && w == 0 && i >= 100 && i < 104 && lane < 14) {
+      if (blockIdx.x == 0 && w == 0 && i >= 100 && i < 104 && lane < 16) {
         unsigned long long t_ = 0;
 #pragma unroll
-        for (int k = 0; k < 14; ++k) t_ = lane == k ? stamp_[k] : t_;
+        for (int k = 0; k < 16; ++k) t_ = lane == k ? stamp_[k] : t_;
         g_v4_stamps[i - 100][lane] = t_;
       }
   }
 
+  if constexpr ((DBG & 128) != 0)
+    if (tid == 0 && blockIdx.x < 2048) g_v4_span[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
   // sample extraction of coefficient 0: mask word t of component comp < K
   // is -ACC[N - t] (t > 0), read reversed through the slot
 #pragma unroll
@@ -1153,6 +1189,8 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
   bool prof = false;
   ProfAcc prof_br, prof_ks;
+  int v4_g = 4;        // v4 ciphertexts per workgroup (FHEICP_V4_G = 1, 2 or 4)
+  int v4_fl = 0;       // v4 per-ciphertext LDS hand-offs instead of s_barrier (FHEICP_V4_FL=1)
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2, 3
   int v4_dbg = 0;      // timing experiments only (FHEICP_V4_DBG), wrong results
   // i8-MFMA key switch: key byte planes and a digit/body workspace
@@ -1269,6 +1307,11 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
     ctx->br_variant = (v == 2 || v == 3 || v == 4) ? v : 4;
   }
   if (const char* e = getenv("FHEICP_V4_DBG")) ctx->v4_dbg = atoi(e);
+  if (const char* e = getenv("FHEICP_V4_G")) {
+    const int g = atoi(e);
+    ctx->v4_g = (g == 1 || g == 2 || g == 4) ? g : 4;
+  }
+  if (const char* e = getenv("FHEICP_V4_FL")) ctx->v4_fl = atoi(e) != 0;
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
   if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
@@ -1299,17 +1342,16 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
     }
     if (N == 1024) {  // v4 per-lane twiddles (br_v4.h), long double
       const long double PI = 3.14159265358979323846264338327950288L;
-      std::vector<c64> t4(v4::NTW * 64);
-      for (int e = 0; e < v4::NTW; ++e)
+      std::vector<c64> t4(v4::NTW);
+      for (int m = 0; m < 8; ++m)
         for (int lane = 0; lane < 64; ++lane) {
-          long double ang;
-          if (e < 8) {
-            ang = PI * (long double)lane * (long double)(1 + 4 * e) / 1024.0L;
-          } else {
-            const int m = e - 7, L = v4::jof(v4::LB, lane, 0) & 7;
-            ang = 2.0L * PI * (long double)(L * m) / 64.0L;
-          }
-          t4[e * 64 + lane] = {(double)cosl(ang), (double)sinl(ang)};
+          const long double ang = PI * (long double)lane * (long double)(1 + 4 * m) / 1024.0L;
+          t4[m * 64 + lane] = {(double)cosl(ang), (double)sinl(ang)};
+        }
+      for (int m = 1; m < 8; ++m)
+        for (int L = 0; L < 8; ++L) {
+          const long double ang = 2.0L * PI * (long double)(L * m) / 64.0L;
+          t4[v4::NTA + (m - 1) * 8 + L] = {(double)cosl(ang), (double)sinl(ang)};
         }
       if (hipMalloc(&ctx->tw4, sizeof(c64) * t4.size()) != hipSuccess ||
           hipMemcpy(ctx->tw4, t4.data(), sizeof(c64) * t4.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1660,14 +1702,24 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,          \
                      p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
 #define BR2(K) do { if (ctx->br_variant == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
-#define BR4(L, A32)                                                                                           \
-  hipLaunchKernelGGL((k_blind_rotate_v4<L, A32>), dim3((unsigned)((count + v4::G - 1) / v4::G)), dim3(v4::NT), 0, \
-                     st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, mode, out, ct_v,          \
-                     refreshed, sign)
-#define BR4D(D)                                                                                               \
-  hipLaunchKernelGGL((k_blind_rotate_v4<2, true, D>), dim3((unsigned)((count + v4::G - 1) / v4::G)), dim3(v4::NT), \
-                     0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, mode, out,               \
-                     ct_v, refreshed, sign)
+#define BR4G(L, A32, D, GG)                                                                                   \
+  if (ctx->v4_fl && GG > 1) BR4F(L, A32, D, GG, true); else BR4F(L, A32, D, GG, false)
+#define BR4F(L, A32, D, GG, FLAGS)                                                                             \
+  hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),       \
+                     dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, \
+                     mode, out, ct_v, refreshed, sign)
+#define BR4(L, A32)                                  \
+  do {                                               \
+    if (ctx->v4_g == 1) BR4G(L, A32, 0, 1);          \
+    else if (ctx->v4_g == 2) BR4G(L, A32, 0, 2);     \
+    else BR4G(L, A32, 0, 4);                         \
+  } while (0)
+#define BR4D(D)                                      \
+  do {                                               \
+    if (ctx->v4_g == 1) BR4G(2, true, D, 1);         \
+    else if (ctx->v4_g == 2) BR4G(2, true, D, 2);    \
+    else BR4G(2, true, D, 4);                        \
+  } while (0)
   if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
       p.pbs_level * p.pbs_base_log <= 31) {
     switch (ctx->v4_dbg) {
@@ -1701,6 +1753,8 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
 #undef BR2
 #undef BR4
 #undef BR4D
+#undef BR4G
+#undef BR4F
 #undef BRV
   prof_end(ctx, ctx->prof_br, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
@@ -2026,6 +2080,7 @@ int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out) {
   if (!h_out) return fail(ctx, FHE_E_ARG, "null output");
   HIPCHK(ctx, hipDeviceSynchronize());
   HIPCHK(ctx, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_v4_stamps), sizeof(unsigned long long) * 64));
+  HIPCHK(ctx, hipMemcpyFromSymbol(h_out + 64, HIP_SYMBOL(g_v4_span), sizeof(unsigned long long) * 2048 * 3));
   return FHE_OK;
 }
 

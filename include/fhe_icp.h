@@ -228,7 +228,9 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
 /* Development aid: 4 x 16 s_memtime phase stamps of one wave of the v4 blind
- * rotation, recorded only when FHEICP_V4_DBG=128 (tools/prof_br.py --stamps). */
+ * rotation, then 2048 x {start, end, HW_ID} per workgroup (s_memrealtime),
+ * recorded only when FHEICP_V4_DBG=128 (tools/prof_br.py --stamps);
+ * h_out holds 64 + 6144 words. */
 int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out);
 
 #ifdef __cplusplus

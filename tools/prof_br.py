@@ -42,14 +42,32 @@ for var, dbg in runs:
     ks = eng.profile_read("keyswitch")
     if dbg == "128":
         import ctypes as C
-        st = np.zeros(64, np.uint64)
+        st = np.zeros(64 + 3 * 2048, np.uint64)
         eng._chk(eng._L.fhe_debug_v4_stamps(eng._ctx, C.c_void_p(st.ctypes.data)))
         names = ["start", "digits", "fwd0", "F0+mac0", "bar1", "mac0x", "bar2", "fwd1", "F1+mac1", "bar3",
                  "mac1x", "bar4", "inverse", "acc"]
         for s4 in range(4):
             row = st[s4 * 16:s4 * 16 + 14].astype(np.int64)
             d = np.diff(row)
-            print("step", 100 + s4, "total", int(row[-1] - row[0]), " ".join(f"{n}:{int(x)}" for n, x in zip(names[1:], d)))
+            rt = int(st[s4 * 16 + 15]) - int(st[s4 * 16 + 14])   # s_memrealtime: 100 MHz
+            clk = (row[-1] - row[0]) / (rt * 10.0) if rt > 0 else 0.0
+            print("step", 100 + s4, "total", int(row[-1] - row[0]), f"realtime_ns {rt * 10} (shader clock ~{clk:.2f} GHz)",
+                  " ".join(f"{n}:{int(x)}" for n, x in zip(names[1:], d)))
+    if dbg == "128":
+        gg = int(os.environ.get("FHEICP_V4_G", "2"))
+        nwg = min(2048, (a.B + gg - 1) // gg)
+        sp = st[64:64 + 3 * nwg].reshape(nwg, 3).astype(np.int64)
+        t0 = sp[:, 0].min()
+        start, end = (sp[:, 0] - t0) * 10, (sp[:, 1] - t0) * 10   # ns at 100 MHz
+        dur = end - start
+        hw = sp[:, 2]
+        cu = (hw >> 8) & 0xF; sh = (hw >> 12) & 1; se = (hw >> 13) & 0x7
+        print(f"workgroups {nwg}: span {end.max() / 1e6:.3f} ms (RTC @100MHz); start min/med/max "
+              f"{start.min() / 1e6:.3f}/{np.median(start) / 1e6:.3f}/{start.max() / 1e6:.3f} ms; "
+              f"duration min/med/max {dur.min() / 1e6:.3f}/{np.median(dur) / 1e6:.3f}/{dur.max() / 1e6:.3f} ms")
+        late = int((start > 0.1 * end.max()).sum())
+        print(f"  workgroups starting after 10% of the span: {late}; distinct (se, sh, cu): "
+              f"{len(set(zip(se.tolist(), sh.tolist(), cu.tolist())))}")
     print(f"variant={var} dbg={dbg} B={a.B} blind_rotate {br['total_ms'] / br['launches']:.3f} ms/launch "
           f"({a.B * br['launches'] / br['total_ms'] * 1e3:.0f} PBS/s), keyswitch {ks['total_ms'] / ks['launches']:.3f} ms/launch")
     eng.close()

@@ -10,7 +10,12 @@ ds_read_b128) it must be bank-conflict-free on gfx950 (MI355X_MICROARCH.md
 lanes of a read group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) 16 distinct
 quads mod 16. Layout LA (natural) is fixed; LB holds index bits 3,4,5 in its
 slots, LC bits 0,1,2. Prints the smallest-scratch solution.
+
+--lb a,b,c,d,e,f fixes LB's lane bits (the kernel now reaches LB from LA in
+registers: slot bits <-> lane bits 3..5, so LB lanes = 0,1,2,6,7,8) and
+searches only LC and the LB <-> LC offsets.
 """
+import sys
 import itertools
 
 BASES = [(0, 0, 0, 0), (1, 2, 4, 8), (0, 1, 2, 4), (1, 1, 2, 4), (2, 4, 8, 16), (0, 2, 4, 8), (1, 2, 4, 7)]
@@ -51,6 +56,18 @@ def best_func(A, B):
 
 
 LA = (0, 1, 2, 3, 4, 5)
+if "--lb" in sys.argv:
+    l2 = tuple(int(x) for x in sys.argv[sys.argv.index("--lb") + 1].split(","))
+    res = []
+    for l3 in itertools.permutations((3, 4, 5, 6, 7, 8)):
+        f2 = best_func(l2, l3)
+        g2 = best_func(l3, l2) if f2 else None
+        if g2:
+            res.append((max(size(f2), size(g2)), l3, f2, g2))
+    sz, l3, f2, g2 = min(res)
+    print("scratch", sz, "LC lanes", l3)
+    print("R2F", f2, "R2I", g2)
+    sys.exit(0)
 best = None
 for l2 in itertools.permutations((0, 1, 2, 6, 7, 8)):
     f1, g1 = best_func(LA, l2), best_func(l2, LA)
