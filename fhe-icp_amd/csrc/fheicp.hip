@@ -1708,10 +1708,12 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),       \
                      dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, \
                      mode, out, ct_v, refreshed, sign)
+// G = 4 needs 3 waves per SIMD (<= 168 VGPRs): only the 32-bit-accumulator
+// kernels; the u64 ones (232 VGPRs, 2 waves per SIMD) run 2 per workgroup.
 #define BR4(L, A32)                                  \
   do {                                               \
     if (ctx->v4_g == 1) BR4G(L, A32, 0, 1);          \
-    else if (ctx->v4_g == 2) BR4G(L, A32, 0, 2);     \
+    else if (ctx->v4_g == 2 || !A32) BR4G(L, A32, 0, 2); \
     else BR4G(L, A32, 0, 4);                         \
   } while (0)
 #define BR4D(D)                                      \
