@@ -904,6 +904,7 @@ __device__ unsigned long long g_v4_span[2048][3];
 // 1 twiddles from a register, 2 no BSK loads, 4 no barriers, 8 no FFT
 // relayout, 16 no LDS rotation, 32 no LDS reads of the other components,
 // 128 phase timestamps (results correct).
+constexpr int FL_SYNC = 1;
 template <int L, bool A32, int DBG = 0, int G = 2, bool FL = false>
 __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
@@ -956,6 +957,11 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
   constexpr int R = WPC * L;
   const c64 wf = {0.5 + (double)beta * 1e-3, (double)L * 1e-3};  // DBG stand-in value
   for (int i = 0; i < n; ++i) {
+    // FL: per-ciphertext hand-offs within a step, but one workgroup barrier
+    // every FL_SYNC steps bounds how far the oldest ciphertext (highest issue
+    // priority) runs ahead of the others
+    if constexpr (FL && (DBG & 4) == 0)
+      if ((i & (FL_SYNC - 1)) == 0) lds_barrier();
     const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)atab[g][i]);
     [[maybe_unused]] unsigned long long stamp_[16];
     V4_STAMP(0);
@@ -1000,12 +1006,14 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
         for (int u = 0; u < S; ++u)
           v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
       }
-      // own-component BSK row: loads fly during the transform (which folds the twist in)
-      c64 kb[S];
-      {
-        const c64* gp = Gi + ((size_t)(comp * L + lv) * WPC + comp) * M;
+      // own-component BSK row: loads fly during the transform (which folds
+      // the twist in); the u64 kernels load it after the transform (VGPRs)
+      constexpr bool PF = A32 || G <= 2;  // u64 kernels at 4 per workgroup: load late (VGPRs)
+      const c64* gpo = Gi + ((size_t)(comp * L + lv) * WPC + comp) * M;
+      c64 kb[PF ? S : 1];
+      if constexpr (PF) {
 #pragma unroll
-        for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gp[u * 64 + lane];
+        for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gpo[u * 64 + lane];
       }
       // FL: the others must have read this slot's previous F before the
       // transform's relayouts overwrite it
@@ -1018,14 +1026,23 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       // own component first (no other wave needed), then the two other rows'
       // BSK loads fly across the barrier
 #pragma unroll
-      for (int u = 0; u < S; ++u) cmac(mac[u], v[u], kb[u]);
-      c64 kx[K][S];
+      for (int u = 0; u < S; ++u) {
+        if constexpr (PF) cmac(mac[u], v[u], kb[u]);
+        else cmac(mac[u], v[u], (DBG & 2) ? c64{wf.x + u, wf.y} : gpo[u * 64 + lane]);
+      }
+      // the other two rows' BSK: A32 kernels issue the loads before the
+      // barrier (they fly across it); the u64-accumulator kernels load them
+      // after it, half a row at a time, to stay within 168 VGPRs (3 waves
+      // per SIMD, 4 ciphertexts per workgroup)
+      c64 kx[PF ? K : 1][PF ? S : 1];
+      if constexpr (PF) {
 #pragma unroll
-      for (int ci = 0; ci < K; ++ci) {
-        const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
-        const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
+        for (int ci = 0; ci < K; ++ci) {
+          const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
+          const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
 #pragma unroll
-        for (int u = 0; u < S; ++u) kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
+          for (int u = 0; u < S; ++u) kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
+        }
       }
       V4_STAMP(3 + 5 * lv);
       if constexpr ((DBG & 4) == 0) {
@@ -1041,13 +1058,18 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       for (int ci = 0; ci < K; ++ci) {
         const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
         const c64* fs = ctslots + cin * SCR;
+        const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {  // F in halves: bounds register use at the peak
-          c64 fv[S / 2];
+          c64 fv[S / 2], kv[S / 2];
 #pragma unroll
-          for (int u = 0; u < S / 2; ++u) fv[u] = (DBG & 32) ? v[hh * 4 + u] : fs[(hh * 4 + u) * 64 + lane];
+          for (int u = 0; u < S / 2; ++u) {
+            fv[u] = (DBG & 32) ? v[hh * 4 + u] : fs[(hh * 4 + u) * 64 + lane];
+            if constexpr (PF) kv[u] = kx[ci][hh * 4 + u];
+            else kv[u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[(hh * 4 + u) * 64 + lane];
+          }
 #pragma unroll
-          for (int u = 0; u < S / 2; ++u) cmac(mac[hh * 4 + u], fv[u], kx[ci][hh * 4 + u]);
+          for (int u = 0; u < S / 2; ++u) cmac(mac[hh * 4 + u], fv[u], kv[u]);
         }
       }
       V4_STAMP(5 + 5 * lv);
@@ -1709,7 +1731,8 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
                      dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, \
                      mode, out, ct_v, refreshed, sign)
 // G = 4 needs 3 waves per SIMD (<= 168 VGPRs): only the 32-bit-accumulator
-// kernels; the u64 ones (232 VGPRs, 2 waves per SIMD) run 2 per workgroup.
+// kernels; the u64 ones (208 VGPRs, 2 waves per SIMD) run 2 per workgroup
+// (at 4 per workgroup they spill: P=21, 22.2 vs 20.9 ms per 1024 PBS).
 #define BR4(L, A32)                                  \
   do {                                               \
     if (ctx->v4_g == 1) BR4G(L, A32, 0, 1);          \
