@@ -241,3 +241,23 @@ def test_pbs_lut_real_vs_oracle(real):
     ph = signed(u64(eng.phase(out)))
     assert np.abs(ph - signed(ref.phase(out_ref))).max() < 2 ** 46
     assert np.abs(ph - (D.astype(np.int64) << 48)).max() < 2 ** 46
+
+
+@pytest.mark.parametrize("g,fl", [("4", "0"), ("4", "1"), ("2", "0"), ("2", "1"), ("1", "0")])
+def test_v4_workgroup_shapes(need_gpu, monkeypatch, g, fl):
+    """Every v4 workgroup shape (FHEICP_V4_G ciphertexts per workgroup, s_barrier
+    or per-ciphertext LDS hand-offs FHEICP_V4_FL) gives the exact sign and
+    refreshed value on the real parameters, with a batch that is not a multiple
+    of the workgroup (B = 1023: the last workgroup runs padding ciphertexts)."""
+    monkeypatch.setenv("FHEICP_V4_G", g)
+    monkeypatch.setenv("FHEICP_V4_FL", fl)
+    eng = Engine(REAL16, 0)
+    eng.keygen(777)
+    h = 2 ** 15
+    v = np.random.default_rng(23).integers(-h, h, 1023)
+    v[:6] = [-h, -1, 0, 1, h - 1, -h + 1]
+    sign = eng.sign(eng.encrypt(v, seed=24))
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    ref_ct, sign2 = eng.bit_extract(eng.encrypt(v[:64], seed=25))
+    assert np.array_equal(eng.decrypt(ref_ct).cpu().numpy(), v[:64])
+    eng.close()
