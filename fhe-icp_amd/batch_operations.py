@@ -97,6 +97,10 @@ class BatchProcessor:
             self._init_model()
         elif self.config.store_ciphertexts and self.config.fhe == "execute":
             self._init_corpus(self.fhe_model)
+        if self.fhe_model is not None and EncryptedDocument.allowed_dims is not None and \
+                self.fhe_model.input_dim not in EncryptedDocument.allowed_dims:
+            EncryptedDocument.allowed_dims = tuple(sorted(set(EncryptedDocument.allowed_dims) |
+                                                          {self.fhe_model.input_dim}))
         self.initial_memory = self._check_memory()
 
     # ------------------------------------------------------------- model --
@@ -111,7 +115,10 @@ class BatchProcessor:
             return
         cfg = self.config
         needs_keys = cfg.fhe == "execute"
-        if cfg.model_path and os.path.exists(cfg.model_path):
+        km_model = self._model_from_key_manager(needs_keys)
+        if km_model is not None:
+            m = km_model
+        elif cfg.model_path and os.path.exists(cfg.model_path):
             m = FHESimilarityModel.load_compiled(cfg.model_path, device=cfg.device) if needs_keys else None
             if m is None:
                 from fheicp import persist
@@ -129,6 +136,26 @@ class BatchProcessor:
         self.fhe_model = m
         if cfg.store_ciphertexts and needs_keys:
             self._init_corpus(m)
+
+    def _model_from_key_manager(self, needs_keys: bool):
+        """The key manager's current key, when it holds fheicp key material
+        (key_management.FHEKeyManager.store_keys): parameters and keys are
+        loaded, not regenerated (§8f-2). None otherwise (a reference key
+        manager, or a key written by the reference)."""
+        km = self.key_manager
+        if km is None or not hasattr(km, "load_key_material"):
+            return None
+        try:
+            if not needs_keys:
+                from fheicp.sklearn import LinearRegression
+                qp, _, _ = km.load_key_material()
+                m = FHESimilarityModel(input_dim=len(qp.coef), n_bits=qp.n_bits, device=self.config.device)
+                m.model = LinearRegression.from_quant_params(qp, device=self.config.device)
+                return m
+            return km.load_compiled(device=self.config.device)
+        except ValueError as e:  # no fheicp material under the current key
+            logger.info("key manager: %s; training a new model", e)
+            return None
 
     def _init_corpus(self, m):
         """Load (config.corpus_path) or create the encrypted-corpus engine."""

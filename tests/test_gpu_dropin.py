@@ -102,3 +102,32 @@ def test_reference_side_ctypes_binding(need_gpu):
         eng.close()
     np.testing.assert_array_equal(acc, acc_ref)
     np.testing.assert_array_equal(below, (acc_ref < T).astype(np.int64))
+
+
+def test_key_manager_generate_load_and_processor(need_gpu, tmp_path):
+    """FHEKeyManager.generate_keys (GPU keygen) -> Fernet-wrapped secret keys +
+    evaluation keys on disk -> a new manager's load_compiled gives the same keys
+    and results, and a BatchProcessor handed the manager uses them instead of
+    retraining (§8f-2), matching the oracle on search."""
+    from batch_operations import BatchConfig, BatchProcessor
+    from encrypted_storage import EncryptedDocument, EncryptedDocumentStore
+    from key_management import FHEKeyManager
+    km = FHEKeyManager(str(tmp_path / "keys"), password="pw")
+    info = km.generate_keys("k16", input_dim=16, n_bits=6, seed=21, key_seed=22)
+    assert km.get_current_key() == "k16" and info["model_file"].endswith("compiled_model.enc")
+    km2 = FHEKeyManager(str(tmp_path / "keys"), password="pw")
+    m = km2.load_compiled()
+    qp, _, keys = km2.load_key_material()
+    X, y = Q.prepare_training_data(16, 1000, seed=21)
+    ref = Q.fit_quantized_linear(X, y, 6)
+    assert ref.to_json() == qp.to_dict()
+    np.testing.assert_array_equal(m.predict_encrypted(X[:64]), Q.predict(ref, X[:64]))
+    exported = m.model._fitted().engine.export_keys()
+    for k in keys:
+        np.testing.assert_array_equal(exported[k], keys[k])
+    cfg = BatchConfig(fhe="execute", input_dim=16, n_bits=6, seed=999, show_progress=False)
+    p = BatchProcessor(key_manager=km2, storage=EncryptedDocumentStore(str(tmp_path / "docs")), config=cfg)
+    assert p.fhe_model.model.quant_params.to_dict() == qp.to_dict()   # loaded, not retrained (seed 999)
+    q, docs = Q.make_corpus(16, 200, seed=14)
+    p.storage.save_many([EncryptedDocument(f"d{i}", "h", "t", docs[i]) for i in range(len(docs))])
+    assert p.search_vector(q, 10, 0.5) == Q.search(ref, q, docs, 10, 0.5, doc_ids=[f"d{i}" for i in range(200)])
