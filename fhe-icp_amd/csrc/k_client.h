@@ -1,0 +1,240 @@
+// Key generation, encryption / decryption and the seeded (stored) corpus kernels.
+// Part of libfheicp (one translation unit: fheicp.hip includes it).
+#pragma once
+
+#include "common.h"
+
+// ============================================================ keygen =======
+__global__ void k_keygen_secrets(ChaKey K, int n, int big, u64* s_small, u64* s_big) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) s_small[i] = stream_word(K, TAG_SK_SMALL, 0, (u64)i) & 1;
+  if (i < big) s_big[i] = stream_word(K, TAG_SK_GLWE, 0, (u64)i) & 1;
+}
+
+// One workgroup per GGSW row (i, r): GLWE_S(0) + s_small[i] * g_lvl on
+// component c_in. body = sum_j A_j * S_j (negacyclic, binary S) + E.
+__global__ void __launch_bounds__(256) k_keygen_bsk(ChaKey K, int N, int k, int L, int beta, int noise_bits,
+                                                    const u64* __restrict__ s_small, const u64* __restrict__ s_big,
+                                                    u64* __restrict__ bsk) {
+  extern __shared__ u64 shm[];
+  u64* A = shm;                                          // N
+  unsigned char* S = (unsigned char*)(shm + N);          // N
+  const int R = (k + 1) * L;
+  const int row = blockIdx.x;  // i * R + r
+  const int i = row / R, r = row % R;
+  const int c_in = r / L, lvl = r % L + 1;
+  u64* dst = bsk + (size_t)row * (k + 1) * N;
+  constexpr int MAXC = 8;  // N <= 2048 -> 8 coefficients per thread
+  u64 body[MAXC];
+  const int per = N / 256;
+  for (int q = 0; q < per; ++q) body[q] = 0;
+  for (int j = 0; j < k; ++j) {
+    const u64 sid = (u64)row * k + j;
+    for (int blk = threadIdx.x; blk < N / 8; blk += 256) {
+      u64 w[8];
+      stream_block(K, TAG_BSK_MASK, sid, (uint32_t)blk, w);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        A[8 * blk + q] = w[q];
+        dst[(size_t)j * N + 8 * blk + q] = w[q];
+      }
+    }
+    for (int t = threadIdx.x; t < N; t += 256) S[t] = (unsigned char)s_big[(size_t)j * N + t];
+    __syncthreads();
+    for (int v = 0; v < N; ++v) {
+      if (!S[v]) continue;  // uniform across the block
+      for (int q = 0; q < per; ++q) {
+        const int t = threadIdx.x + 256 * q;
+        body[q] += (t >= v) ? A[t - v] : (u64)0 - A[t - v + N];
+      }
+    }
+    __syncthreads();
+  }
+  for (int q = 0; q < per; ++q) {
+    const int t = threadIdx.x + 256 * q;
+    u64 b = body[q] + (u64)tuniform(stream_word(K, TAG_BSK_NOISE, (u64)row, (u64)t), noise_bits);
+    dst[(size_t)k * N + t] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_small[i]) dst[(size_t)c_in * N] += 1ull << (64 - lvl * beta);
+}
+
+// One workgroup per KSK row (i, l): LWE_{s_small}(s_big[i] * 2^(64 - (l+1) beta)).
+__global__ void __launch_bounds__(256) k_keygen_ksk(ChaKey K, int n, int KL, int kbeta, int noise_bits,
+                                                    const u64* __restrict__ s_small, const u64* __restrict__ s_big,
+                                                    u64* __restrict__ ksk) {
+  __shared__ u64 red[4];
+  const int row = blockIdx.x;  // i * KL + l
+  const int i = row / KL, l = row % KL;
+  u64* dst = ksk + (size_t)row * (n + 1);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < (n + 7) / 8; blk += 256) {
+    u64 w[8];
+    stream_block(K, TAG_KSK_MASK, (u64)row, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int t = 8 * blk + q;
+      if (t < n) {
+        dst[t] = w[q];
+        if (s_small[t]) part += w[q];
+      }
+    }
+  }
+  const u64 s = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    u64 b = s + (u64)tuniform(stream_word(K, TAG_KSK_NOISE, (u64)row, 0), noise_bits);
+    if (s_big[i]) b += 1ull << (64 - (l + 1) * kbeta);
+    dst[n] = b;
+  }
+}
+
+// One wave per polynomial: fold/twist, forward FFT, scale 1/M, store in the
+// [u][lane] order the blind rotation reads (coalesced 1 KiB per slot).
+template <int LOGM>
+__global__ void __launch_bounds__(64) k_bsk_to_fft(const u64* __restrict__ bsk, int npoly,
+                                                   const c64* __restrict__ tw, const c64* __restrict__ twist,
+                                                   c64* __restrict__ out) {
+  using F = WaveFFT<LOGM>;
+  constexpr int M = F::M, S = F::S;
+  __shared__ c64 lds[F::LDS_ELEMS];
+  const int poly = blockIdx.x, l = threadIdx.x;
+  if (poly >= npoly) return;
+  const u64* src = bsk + (size_t)poly * 2 * M;
+  c64 v[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) {
+    const int t = l + 64 * u;
+    const c64 a = {(double)(int64_t)src[t], (double)(int64_t)src[t + M]};
+    v[u] = cmul(a, twist[t]);
+  }
+  F::forward(v, tw, lds, l);
+  const double inv = 1.0 / (double)M;
+  c64* dst = out + (size_t)poly * M;
+#pragma unroll
+  for (int u = 0; u < S; ++u) dst[u * 64 + l] = {v[u].x * inv, v[u].y * inv};
+}
+
+// ============================================================ client =======
+// One workgroup (256 threads) per ciphertext of dimension `dim` (multiple of 8).
+__global__ void __launch_bounds__(256) k_encrypt(ChaKey K, int dim, int msg_bits, int noise_bits,
+                                                 const u64* __restrict__ s_big, const int64_t* __restrict__ msg,
+                                                 u64 id0, u64* __restrict__ ct) {
+  __shared__ u64 red[4];
+  const int64_t c = blockIdx.x;
+  const u64 id = id0 + (u64)c;
+  u64* o = ct + (size_t)c * (dim + 1);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 w[8];
+    stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[8 * blk + q] = w[q];
+      part += w[q] & (0 - s_big[8 * blk + q]);
+    }
+  }
+  const u64 s = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    const u64 e = (u64)tuniform(stream_word(K, TAG_ENC_NOISE, id, 0), noise_bits);
+    o[dim] = s + e + ((u64)msg[c] << (64 - msg_bits));
+  }
+}
+
+// ---- seeded (compressed) ciphertexts: the stored document corpus ----------
+// A seeded LWE keeps only its body; the mask is stream(TAG_ENC_MASK, id) of
+// a PUBLIC mask key Km, the noise stream(TAG_ENC_NOISE, id) of a SECRET
+// noise key Kn. Document b of a corpus holds D bodies,
+// feature j under stream id id0[b] + j. 2049 -> 1 word per feature in HBM:
+// the masks are regenerated where they are consumed (k_linear_seeded).
+__global__ void __launch_bounds__(256) k_encrypt_seeded(ChaKey Km, ChaKey Kn, int dim, int msg_bits, int noise_bits,
+                                                        const u64* __restrict__ s_big,
+                                                        const int64_t* __restrict__ msg,
+                                                        const u64* __restrict__ id0, int D, u64* __restrict__ body) {
+  __shared__ u64 red[4];
+  const int64_t c = blockIdx.x;
+  const int64_t b = c / D;
+  const u64 id = id0[b] + (u64)(c - b * D);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 w[8];
+    stream_block(Km, TAG_ENC_MASK, id, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) part += w[q] & (0 - s_big[8 * blk + q]);
+  }
+  const u64 s = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    const u64 e = (u64)tuniform(stream_word(Kn, TAG_ENC_NOISE, id, 0), noise_bits);
+    body[c] = s + e + ((u64)msg[c] << (64 - msg_bits));
+  }
+}
+
+// full ciphertexts [B*D][dim+1] from the seeded corpus (interop / tests)
+__global__ void __launch_bounds__(256) k_expand_seeded(ChaKey Km, int dim, const u64* __restrict__ body,
+                                                       const u64* __restrict__ id0, int D, u64* __restrict__ ct) {
+  const int64_t c = blockIdx.x;
+  const int64_t b = c / D;
+  const u64 id = id0[b] + (u64)(c - b * D);
+  u64* o = ct + (size_t)c * (dim + 1);
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 w[8];
+    stream_block(Km, TAG_ENC_MASK, id, (uint32_t)blk, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[8 * blk + q] = w[q];
+  }
+  if (threadIdx.x == 0) o[dim] = body[c];
+}
+
+// out[b] = sum_j w[j] * ct(b, j) + cst * Delta on the seeded corpus: one
+// workgroup per document, each thread owns one 8-word ChaCha block of the
+// mask (dim / 8 threads), regenerated per feature in registers. Reads D + 1
+// words per document from HBM instead of D (dim + 1).
+__global__ void __launch_bounds__(256) k_linear_seeded(ChaKey Km, int dim, const u64* __restrict__ body,
+                                                       const u64* __restrict__ id0, int D,
+                                                       const int64_t* __restrict__ w, u64 cst_scaled,
+                                                       u64* __restrict__ out) {
+  const int64_t b = blockIdx.x;
+  const u64 base = id0[b];
+  u64* o = out + (size_t)b * (dim + 1);
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < D; ++j) {
+      u64 m[8];
+      stream_block(Km, TAG_ENC_MASK, base + (u64)j, (uint32_t)blk, m);
+      const u64 wj = (u64)w[j];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * m[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[8 * blk + q] = acc[q];
+  }
+  if (threadIdx.x == 0) {
+    u64 acc = cst_scaled;
+    for (int j = 0; j < D; ++j) acc += (u64)w[j] * body[(size_t)b * D + j];
+    o[dim] = acc;
+  }
+}
+
+// mode 0: decode signed msg_bits integer; 1: bit (nearer 2^63); 2: raw phase
+__global__ void __launch_bounds__(256) k_decrypt(int dim, int msg_bits, int mode, const u64* __restrict__ s,
+                                                 const u64* __restrict__ ct, int64_t* __restrict__ out) {
+  __shared__ u64 red[4];
+  const int64_t c = blockIdx.x;
+  const u64* x = ct + (size_t)c * (dim + 1);
+  u64 part = 0;
+  for (int t = threadIdx.x; t < dim; t += 256) part += x[t] & (0 - s[t]);
+  const u64 sum = block_sum_u64<256>(part, red);
+  if (threadIdx.x == 0) {
+    const u64 ph = x[dim] - sum;
+    int64_t r;
+    if (mode == 0) {
+      u64 q = ((ph >> (63 - msg_bits)) + 1) >> 1;
+      if (msg_bits < 64) q &= (1ull << msg_bits) - 1;
+      r = (q >> (msg_bits - 1)) ? (int64_t)q - ((int64_t)1 << msg_bits) : (int64_t)q;
+    } else if (mode == 1) {
+      r = (int64_t)(((ph + (1ull << 62)) >> 63) & 1);
+    } else {
+      r = (int64_t)ph;
+    }
+    out[c] = r;
+  }
+}

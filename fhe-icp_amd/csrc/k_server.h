@@ -1,0 +1,302 @@
+// Server-side kernels: leveled linear layer, key switch (VALU and i8 MFMA), quantisation, top-k.
+// Part of libfheicp (one translation unit: fheicp.hip includes it).
+#pragma once
+
+#include "common.h"
+
+// ============================================================ server =======
+// out[b][t] = sum_j w[j] ct[b][j][t] (+ cst * Delta on the body)
+__global__ void __launch_bounds__(256) k_linear(const u64* __restrict__ ct, int D, int W,
+                                                const int64_t* __restrict__ w, u64 cst_scaled,
+                                                u64* __restrict__ out) {
+  const int64_t b = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= W) return;
+  const u64* x = ct + (size_t)b * D * W + t;
+  u64 acc = 0;
+  for (int j = 0; j < D; ++j) acc += (u64)w[j] * x[(size_t)j * W];
+  if (t == W - 1) acc += cst_scaled;
+  out[(size_t)b * W + t] = acc;
+}
+
+// Key switch (big -> small key), as a split-K integer GEMM:
+//   out[c][t] = body_c + (B/2) colsum[t] - sum_{i,l} d'[c][i][l] * KSK[i][l][t]
+// with offset-binary digits d' = d + B/2 in [0, B) (so each term is two
+// v_mad_u64_u32 on the 32-bit halves of the KSK word) and
+// colsum[t] = sum over all rows of KSK[.][t] (precomputed at keygen).
+// Workgroup = KS_TC ciphertexts x 256 output columns x one slice of the
+// input rows; slices are combined with u64 atomics, which are exact and
+// order-independent modulo 2^64 (bit-identical results every run).
+constexpr int KS_TC = 16, KS_IC = 32, KS_SPLIT = 8;
+__global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, int64_t count, int big, int n,
+                                                   int KL, int kbeta, int shift, u64 add_body,
+                                                   const u64* __restrict__ ksk, const u64* __restrict__ colsum,
+                                                   u64* __restrict__ out) {
+  __shared__ uint8_t dig[KS_IC][8][KS_TC];  // [input][level][ciphertext]
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.y * KS_TC;
+  const int nct = (int)min((int64_t)KS_TC, count - c0);
+  const int per = (big + KS_SPLIT - 1) / KS_SPLIT;
+  const int ibeg = blockIdx.z * per, iend_all = min(big, ibeg + per);
+  const u64 half = 1ull << (kbeta - 1);
+  u64 lo[KS_TC], hi[KS_TC];
+#pragma unroll
+  for (int q = 0; q < KS_TC; ++q) lo[q] = hi[q] = 0;
+  for (int i0 = ibeg; i0 < iend_all; i0 += KS_IC) {
+    for (int e = threadIdx.x; e < KS_TC * KS_IC; e += 256) {
+      const int q = e / KS_IC, ii = e % KS_IC;
+      if (q < nct && i0 + ii < iend_all) {
+        const u64 a = in[(size_t)(c0 + q) * (big + 1) + i0 + ii] << shift;
+        const u64 packed = decompose_packed(a, kbeta, KL);  // offset-binary already
+        for (int l = 1; l <= KL; ++l) dig[ii][l - 1][q] = (uint8_t)((packed >> ((KL - l) * kbeta)) & ((1u << kbeta) - 1));
+      } else {
+        for (int l = 0; l < KL; ++l) dig[ii][l][q] = (uint8_t)half;  // digit 0
+      }
+    }
+    __syncthreads();
+    if (col <= n) {
+      const int cnt = min(KS_IC, iend_all - i0);
+      for (int ii = 0; ii < cnt; ++ii) {
+        for (int l = 0; l < KL; ++l) {
+          const u64 kv = ksk[((size_t)(i0 + ii) * KL + l) * (n + 1) + col];
+          const uint32_t kl = (uint32_t)kv, kh = (uint32_t)(kv >> 32);
+          const uint32_t* d4 = (const uint32_t*)&dig[ii][l][0];
+#pragma unroll
+          for (int w = 0; w < KS_TC / 4; ++w) {
+            const uint32_t pk = d4[w];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const uint32_t d = (pk >> (8 * b)) & 0xFF;
+              lo[4 * w + b] += (u64)d * kl;
+              hi[4 * w + b] += (u64)d * kh;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (col <= n) {
+#pragma unroll
+    for (int q = 0; q < KS_TC; ++q) {
+      if (q < nct) {
+        u64 v = (u64)0 - (lo[q] + (hi[q] << 32));
+        if (blockIdx.z == 0) {
+          v += half * colsum[col];
+          if (col == n) v += (in[(size_t)(c0 + q) * (big + 1) + big] << shift) + add_body;
+        }
+        atomicAdd((unsigned long long*)&out[(size_t)(c0 + q) * (n + 1) + col], (unsigned long long)v);
+      }
+    }
+  }
+}
+
+// colsum[t] = sum over all KSK rows of KSK[row][t] (mod 2^64)
+__global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, u64* __restrict__ colsum) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > n) return;
+  u64 s = 0;
+  for (int r = 0; r < rows; ++r) s += ksk[(size_t)r * (n + 1) + t];
+  colsum[t] = s;
+}
+
+// Test vector of a bootstrap: TV_j = base + (j >> shift) * step for
+// j in [0, N) (a staircase; step = 0 gives the constant TV of a sign
+// bootstrap), extended negacyclically: coefficient t of X^{-b} TV is
+// TV_{(t+b) mod 2N} with a minus sign when (t + b) mod 2N >= N.
+// ---- key switch on the i8 matrix cores (v_mfma_i32_16x16x64_i8) ----------
+// out[c] = (0, .., 0, b'[c]) - sum_r D[c][r] * KSK[r], r = i * ks_level + l,
+// a GEMM [count x K] (digits in [-2^(b-1), 2^(b-1))) x [K x (n+1)] over
+// Z_2^64. The key is split into 8 balanced radix-256 byte planes,
+// KSK = sum_q s_q 2^(8q) with s_q in [-128, 127], each an i8 GEMM with i32
+// accumulation (|sum| <= K * 2^(b-1) * 128 < 2^31); the epilogue recombines
+// sum_q acc_q << 8q modulo 2^64 (exact: DESIGN.md §4.3).
+// Fragment layouts (checked by tools/mfma_i8_probe.hip): lane l holds
+// A[row l&15][k = 16 (l>>4) + j] and B[k = 16 (l>>4) + j][col l&15] in byte j;
+// C/D: row 4 (l>>4) + reg, col l&15.
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int KSM_NB_COLS = 16;  // columns per block
+
+// key planes: [kb][nb][q][lane][16 B]
+__global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int n1, int NB, int8_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)K * NB * 16) return;
+  const int row = (int)(e / (NB * 16)), col = (int)(e % (NB * 16));
+  u64 x = col < n1 ? ksk[(size_t)row * n1 + col] : 0;
+  const int kb = row >> 6, g = (row >> 4) & 3, j = row & 15;
+  const int nb = col >> 4, lane = (col & 15) + 16 * g;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int8_t sq = (int8_t)(x & 0xff);
+    x = (x - (u64)(int64_t)sq) >> 8;
+    out[((((size_t)kb * NB + nb) * 8 + q) * 64 + lane) * 16 + j] = sq;
+  }
+}
+
+// digits in A-fragment order [cb][kb][lane][16 B] (ks_level = 4: a
+// coefficient's 4 digits are 4 consecutive bytes) and b' = (b << shift) + add
+__global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, int64_t count, int big, int beta,
+                                                   int shift, u64 add_body, int KB, uint32_t* __restrict__ D,
+                                                   u64* __restrict__ body) {
+  const int t = threadIdx.x, cl = t >> 4, il = t & 15;
+  const int64_t cb = blockIdx.y, c = cb * 16 + cl;
+  const int kb = blockIdx.x, i = kb * 16 + il;
+  if (c >= count) return;
+  const u64* src = in + (size_t)c * (big + 1);
+  if (kb == 0 && il == 0) body[c] = (src[big] << shift) + add_body;
+  const int prec = 4 * beta;
+  uint32_t r = (uint32_t)((((src[i] << shift) >> (63 - prec)) + 1) >> 1);
+  uint32_t packed = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {  // LSB-first; level l = 3 - s sits in byte l
+    const int d = __builtin_amdgcn_sbfe((int)r, s * beta, beta);
+    r -= (uint32_t)d << (s * beta);
+    packed |= (uint32_t)(uint8_t)(int8_t)d << (8 * (3 - s));
+  }
+  const int lane = cl + 16 * (il >> 2);
+  D[(((size_t)cb * KB + kb) * 64 + lane) * 4 + (il & 3)] = packed;
+}
+
+// workgroup = 4 waves = 64 ciphertexts x 16 columns x 8 byte planes; the key
+// tile of each k-block (8 KB) is shared through double-buffered LDS
+__global__ void __launch_bounds__(256) k_keyswitch_mfma(const v4i* __restrict__ D, const v4i* __restrict__ K8,
+                                                        const u64* __restrict__ body, int64_t count, int n1, int NB,
+                                                        int KB, u64* __restrict__ out) {
+  __shared__ v4i bt[2][8 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nb = blockIdx.y;
+  const int64_t cb = (int64_t)blockIdx.x * 4 + w;
+  const bool act = cb * 16 < count;
+  const v4i zero = {0, 0, 0, 0};
+  const v4i* Dv = D + (size_t)cb * KB * 64 + lane;
+  const v4i* Kv = K8 + (size_t)nb * 8 * 64;
+  v4i acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = zero;
+  bt[0][tid] = Kv[tid];
+  bt[0][tid + 256] = Kv[tid + 256];
+  v4i a = act ? Dv[0] : zero;
+  __syncthreads();
+  for (int kb = 0; kb < KB; ++kb) {
+    const int cur = kb & 1;
+    v4i n0 = zero, n1v = zero, an = zero;
+    const bool more = kb + 1 < KB;
+    if (more) {
+      const v4i* srcp = Kv + (size_t)(kb + 1) * NB * 8 * 64;
+      n0 = srcp[tid];
+      n1v = srcp[tid + 256];
+      if (act) an = Dv[(size_t)(kb + 1) * 64];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bt[cur][q * 64 + lane], acc[q], 0, 0, 0);
+    if (more) {
+      bt[cur ^ 1][tid] = n0;
+      bt[cur ^ 1][tid + 256] = n1v;
+      a = an;
+    }
+    __syncthreads();
+  }
+  if (!act) return;
+  const int col = nb * KSM_NB_COLS + (lane & 15);
+  if (col >= n1) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t c = cb * 16 + 4 * (lane >> 4) + r;
+    if (c >= count) continue;
+    u64 v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += (u64)(int64_t)acc[q][r] << (8 * q);
+    out[(size_t)c * n1 + col] = (col == n1 - 1 ? body[c] : (u64)0) - v;
+  }
+}
+
+// Blind rotation + sample extraction. One 64-lane wavefront (= workgroup)
+// per ciphertext; the GLWE accumulator ((K+1) x N u64) lives in LDS, the
+// external-product partial sums in registers.
+// Test vector and epilogue modes: BrTv / br_emit above.
+
+template <typename QT, typename DT>
+__global__ void k_pair_quantize(const QT* __restrict__ query, const DT* __restrict__ docs, int64_t B, int D,
+                                double scale, double zp, double qmin, double qmax, int64_t* __restrict__ qx) {
+  using RT = decltype(QT() * DT());  // numpy promotion of the element-wise product
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * D) return;
+  const RT x = query ? (RT)query[e % D] * (RT)docs[e] : (RT)docs[e];
+  double q = rint((double)x / scale + zp);
+  q = fmin(fmax(q, qmin), qmax);
+  qx[e] = (int64_t)q;
+}
+
+// score[b] = out_scale * double(acc[b])  (UniformQuantizer.dequant, zp 0)
+__global__ void k_dequantize(const int64_t* __restrict__ acc, int64_t B, double out_scale, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) out[i] = out_scale * (double)acc[i];
+}
+
+
+__global__ void k_add_scalar(const int64_t* __restrict__ v, int64_t B, int64_t T, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) out[i] = v[i] + T;
+}
+
+// Single-workgroup top-k by (acc desc, idx asc) over entries not below the
+// threshold. k passes; pass p selects the largest key strictly smaller than
+// the key chosen in pass p-1 (keys are unique because indices are).
+__global__ void __launch_bounds__(1024) k_topk(const int64_t* __restrict__ accv, const int64_t* __restrict__ below,
+                                               int64_t B, int64_t base_idx, int kk, int64_t* __restrict__ oa,
+                                               int64_t* __restrict__ oi) {
+  __shared__ int64_t sa[16], si[16];
+  __shared__ int64_t last_a, last_i;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) {
+    last_a = INT64_MAX;
+    last_i = -1;
+  }
+  __syncthreads();
+  for (int p = 0; p < kk; ++p) {
+    const int64_t la = last_a, li = last_i;
+    int64_t ba = INT64_MIN, bi = -1;
+    for (int64_t x = tid; x < B; x += 1024) {
+      if (below && below[x]) continue;
+      const int64_t a = accv[x];
+      // strictly after (la, li) in (acc desc, idx asc) order
+      const bool after = (a < la) || (a == la && x > li);
+      if (!after) continue;
+      if (bi < 0 || a > ba || (a == ba && x < bi)) {
+        ba = a;
+        bi = x;
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t oa2 = __shfl_down(ba, off, 64), oi2 = __shfl_down(bi, off, 64);
+      if (oi2 >= 0 && (bi < 0 || oa2 > ba || (oa2 == ba && oi2 < bi))) {
+        ba = oa2;
+        bi = oi2;
+      }
+    }
+    if (lane == 0) {
+      sa[w] = ba;
+      si[w] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t fa = INT64_MIN, fi = -1;
+      for (int q = 0; q < 16; ++q) {
+        if (si[q] >= 0 && (fi < 0 || sa[q] > fa || (sa[q] == fa && si[q] < fi))) {
+          fa = sa[q];
+          fi = si[q];
+        }
+      }
+      oa[p] = fi >= 0 ? fa : INT64_MIN;
+      oi[p] = fi >= 0 ? fi + base_idx : -1;
+      if (fi >= 0) {
+        last_a = fa;
+        last_i = fi;
+      } else {
+        last_a = INT64_MIN;  // nothing left: every later pass finds nothing
+        last_i = INT64_MAX;
+      }
+    }
+    __syncthreads();
+  }
+}
