@@ -109,21 +109,30 @@ def br_flops_per_ct(p) -> float:
 def roofline(p, br) -> dict:
     """External-product (blind rotation) kernel roofline from the HIP events
     bracketing every launch on its stream (fhe_profile_read)."""
+    from dataclasses import replace
+    from fheicp.params import sign_plan, sign_rounds
     avg_ms = br["total_ms"] / max(br["launches"], 1)
     cts_per_launch = br["items"] / max(br["launches"], 1)
-    R = (p.k + 1) * p.pbs_level
-    bsk_bytes = p.n * R * (p.k + 1) * (p.N // 2) * 16
+    # launch mix: with a fast gadget, sign_plan's j of every R bootstraps run
+    # on the main gadget and the rest on the fast one (same launch count)
+    mix = [(1.0, p)]
+    if p.pbs_fast_level and p.msg_bits >= 4:
+        d, j = sign_plan(p)
+        R_all = len(sign_rounds(p.msg_bits, d))
+        mix = [(j / R_all, p), (1 - j / R_all, replace(p, pbs_base_log=p.pbs_fast_base_log,
+                                                       pbs_level=p.pbs_fast_level))]
+    bsk_bytes = sum(w * q.n * (q.k + 1) * q.pbs_level * (q.k + 1) * (q.N // 2) * 16 for w, q in mix)
     io_bytes = cts_per_launch * ((p.n + 1) * 8 + (p.k * p.N + 1) * 8 * 5)
     alg_bytes = bsk_bytes + io_bytes
     achieved_gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
-    flops = br_flops_per_ct(p) * cts_per_launch
+    flops = sum(w * br_flops_per_ct(q) for w, q in mix) * cts_per_launch
     achieved_tf = flops / (avg_ms * 1e-3) / 1e12
     traffic = None
     tj = REPO / "profiles" / "r01_br_traffic.json"
     if tj.exists():
         try:
             tr = json.loads(tj.read_text())
-            if tr.get("pbs_level", p.pbs_level) == p.pbs_level:
+            if tr.get("pbs_level", p.pbs_level) == p.pbs_level and not p.pbs_fast_level:
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -40,6 +41,8 @@ struct fhe_ctx {
   bool keys = false;
   u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
   c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr, *tw4 = nullptr;
+  u64* bsk2 = nullptr;      // fast-gadget bootstrapping key (p.pbs_fast_*), coefficient domain
+  c64* bsk2_fft = nullptr;  // ... and its FFT form
   // workspace
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -97,36 +100,98 @@ static int validate(const fhe_params* p, std::string& why) {
   if (p->sign_digit_bits != 0 && (p->sign_digit_bits < 3 || p->sign_digit_bits > 4)) {
     why = "sign_digit_bits must be 0 (auto), 3 or 4"; return -1;
   }
+  if ((p->pbs_fast_base_log == 0) != (p->pbs_fast_level == 0) || p->pbs_fast_level < 0 || p->pbs_fast_level > 8 ||
+      p->pbs_fast_base_log < 0 || p->pbs_fast_level * p->pbs_fast_base_log > 62) {
+    why = "fast pbs decomposition out of range (0, 0 for none)"; return -1;
+  }
   return 0;
 }
 
 static double tuniform_var(int b) { return (std::ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
 
+// Noise model, the same formulas as fheicp/params.py and
+// oracle/tfhe_ref.c; variances relative to the 2^64 torus.
+static double pbs_var(const fhe_params& p, int beta, int L) {
+  const double s2_bsk = tuniform_var(p.glwe_noise_bits) / std::ldexp(1.0, 128);
+  const double B = std::ldexp(1.0, beta);
+  const double rows = (double)L * (p.k + 1) * p.N;
+  return p.n * rows * (B * B + 2) / 12.0 * s2_bsk + p.n * (1 + p.k * p.N / 2.0) / (12.0 * std::pow(B, 2.0 * L));
+}
+static double ks_var(const fhe_params& p) {
+  const double s2_ksk = tuniform_var(p.lwe_noise_bits) / std::ldexp(1.0, 128);
+  const double Bk = std::ldexp(1.0, p.ks_base_log);
+  return (double)p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk +
+         p.k * p.N / 2.0 * std::ldexp(1.0, -2 * p.ks_level * p.ks_base_log) / 12.0;
+}
+static double ms_var(const fhe_params& p) { return (p.n / 2.0 + 1) / 12.0 / ((2.0 * p.N) * (2.0 * p.N)); }
+
 // Decision margin in sigmas of the worst round of a d-bit digit sign
-// extraction: the staircase round of the lowest digit, margin 2^-(d+1) of the
-// torus, the preceding bootstrap's noise amplified by 2^(P-d), plus key
-// switch and modulus switch noise. Same model as fheicp/params.py
-// noise_report.
+// extraction on one gadget: the staircase round of the lowest digit, margin
+// 2^-(d+1) of the torus, the preceding bootstrap's noise amplified by
+// 2^(P-d), plus key switch and modulus switch noise.
 static double digit_margin_sigmas(const fhe_params& p, int d) {
-  const double q2 = std::ldexp(1.0, 128);
-  const double s2_bsk = tuniform_var(p.glwe_noise_bits) / q2, s2_ksk = tuniform_var(p.lwe_noise_bits) / q2;
-  const double B = std::ldexp(1.0, p.pbs_base_log), Bk = std::ldexp(1.0, p.ks_base_log);
-  const double rows = (double)p.pbs_level * (p.k + 1) * p.N;
-  const double v_pbs = p.n * rows * (B * B + 2) / 12.0 * s2_bsk +
-                       p.n * (1 + p.k * p.N / 2.0) / (12.0 * std::pow(B, 2.0 * p.pbs_level));
-  const double v_ks = (double)p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk +
-                      p.k * p.N / 2.0 * std::ldexp(1.0, -2 * p.ks_level * p.ks_base_log) / 12.0;
-  const double v_ms = (p.n / 2.0 + 1) / 12.0 / ((2.0 * p.N) * (2.0 * p.N));
-  const double v = v_pbs * std::ldexp(1.0, 2 * (p.msg_bits - d)) + v_ks + v_ms;
+  const double v = pbs_var(p, p.pbs_base_log, p.pbs_level) * std::ldexp(1.0, 2 * (p.msg_bits - d)) + ks_var(p) +
+                   ms_var(p);
   return std::ldexp(1.0, -(d + 1)) / std::sqrt(v);
 }
 
+// The bootstraps of fhe_sign_batch in order, as (shift, log2 margin): the
+// round reads v << shift, and every earlier bootstrap output subtracted from
+// v is amplified by 2^shift.
+static int sign_rounds(int P, int d, int* shift, int* mlog) {
+  int R = 0, b = 0;
+  const int m = P - d;
+  auto add = [&](int sh, int ml) { shift[R] = sh; mlog[R] = ml; ++R; };
+  for (; b + d <= m; b += d) { add(P - b - d, -(d + 1)); add(P - b - d, -(d + 1)); }
+  if (m - b >= 3) { const int c = m - b; add(P - b - c, -(c + 1)); add(P - b - c, -(c + 1)); b = m; }
+  for (; b < m; ++b) add(P - b - 1, -2);
+  add(0, -(d + 1));
+  return R;
+}
+// worst margin (sigmas) over all rounds when rounds < j use the main gadget
+static double plan_worst(const fhe_params& p, int d, int j) {
+  int sh[64], ml[64];
+  const int R = sign_rounds(p.msg_bits, d, sh, ml);
+  const double vm = pbs_var(p, p.pbs_base_log, p.pbs_level), vf = pbs_var(p, p.pbs_fast_base_log, p.pbs_fast_level);
+  const double fixed = ks_var(p) + ms_var(p);
+  double acc = 0, worst = 1e300;
+  for (int r = 0; r < R; ++r) {
+    worst = std::min(worst, std::ldexp(1.0, ml[r]) / std::sqrt(acc * std::ldexp(1.0, 2 * sh[r]) + fixed));
+    acc += r < j ? vm : vf;
+  }
+  return worst;
+}
+// (d, j): digit width and how many leading bootstraps need the main gadget.
+// Without a fast gadget: the single-gadget rule (d = 4 if its worst round
+// keeps 9.2 sigma, else 3), all rounds on the main gadget. With one: the
+// widest d (or the forced one) and the fewest main-gadget rounds for which
+// every round keeps 9.2 sigma.
+static void sign_plan(const fhe_params& p, int* d_out, int* j_out) {
+  int sh[64], ml[64];
+  const int P = p.msg_bits;
+  if (P < 4) { *d_out = 0; *j_out = P; return; }
+  if (!p.pbs_fast_level) {
+    int d = 3;
+    if (p.sign_digit_bits) d = std::min(p.sign_digit_bits, P);
+    else if (digit_margin_sigmas(p, std::min(4, P)) >= 9.2) d = std::min(4, P);
+    *d_out = d;
+    *j_out = sign_rounds(P, d, sh, ml);
+    return;
+  }
+  const int first = p.sign_digit_bits ? std::min(p.sign_digit_bits, P) : std::min(4, P);
+  const int last = p.sign_digit_bits ? first : 3;
+  for (int d = first; d >= last; --d) {
+    const int R = sign_rounds(P, d, sh, ml);
+    for (int j = 0; j <= R; ++j)
+      if (plan_worst(p, d, j) >= 9.2) { *d_out = d; *j_out = j; return; }
+  }
+  *d_out = last;
+  *j_out = sign_rounds(P, last, sh, ml);
+}
 static int sign_digits(const fhe_params& p) {
-  if (p.msg_bits < 4) return 0;
-  if (p.sign_digit_bits) return std::min(p.sign_digit_bits, (int)p.msg_bits);
-  for (int d = std::min(4, (int)p.msg_bits); d > 3; --d)
-    if (digit_margin_sigmas(p, d) >= 9.2) return d;
-  return 3;
+  int d, j;
+  sign_plan(p, &d, &j);
+  return d;
 }
 
 extern "C" {
@@ -173,9 +238,7 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
   // (measured: v4 wins at gadget levels <= 3, e.g. 21.6 vs 23.6 ms at P=21; from
   // level 4 its 64-bit accumulator spills and v2 is faster, 40.6 vs 53.0 ms at P=26)
-  if (ctx->br_variant == 4 && !(params->k == 2 && params->n <= v4::NMAX && params->pbs_level <= 3 &&
-                                 (params->pbs_level == 1 || params->pbs_base_log <= 16)))
-    ctx->br_variant = 2;
+  // (the choice is per gadget: variant_for)
   if (device >= 0) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
@@ -241,6 +304,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     hipSetDevice(ctx->device);
     hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk); hipFree(ctx->ksk_colsum);
     hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
+    hipFree(ctx->bsk2); hipFree(ctx->bsk2_fft);
     hipFree(ctx->ksk8); hipFree(ctx->ks_ws); hipFree(ctx->tw4);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_ks);
@@ -271,8 +335,28 @@ static int need_keys(fhe_ctx* ctx) {
   return FHE_OK;
 }
 
+// blind-rotation kernel for a gadget: the requested variant (4 unless
+// FHEICP_BR_VARIANT), falling back to v2 where v4 does not apply
+static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
+  if (ctx->br_variant == 4 &&
+      !(q.k == 2 && q.n <= v4::NMAX && q.pbs_level <= 3 && (q.pbs_level == 1 || q.pbs_base_log <= 16)))
+    return 2;
+  return ctx->br_variant;
+}
+// the parameters seen through the fast gadget (same keys, other decomposition)
+static fhe_params fast_params(const fhe_params& p) {
+  fhe_params q = p;
+  q.pbs_base_log = p.pbs_fast_base_log;
+  q.pbs_level = p.pbs_fast_level;
+  return q;
+}
 static int alloc_keys(fhe_ctx* ctx) {
   const fhe_params& p = ctx->p;
+  if (p.pbs_fast_level && !ctx->bsk2) {
+    const fhe_params q = fast_params(p);
+    HIPCHK(ctx, hipMalloc(&ctx->bsk2, 8 * fhe_bsk_words(&q)));
+    HIPCHK(ctx, hipMalloc(&ctx->bsk2_fft, sizeof(c64) * fhe_bsk_words(&q) / 2));
+  }
   if (ctx->s_small) return FHE_OK;
   HIPCHK(ctx, hipMalloc(&ctx->s_small, 8 * (size_t)p.n));
   HIPCHK(ctx, hipMalloc(&ctx->s_big, 8 * (size_t)p.k * p.N));
@@ -283,6 +367,23 @@ static int alloc_keys(fhe_ctx* ctx) {
   return FHE_OK;
 }
 
+static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* bsk_fft, hipStream_t st) {
+  const int npoly = (int)(fhe_bsk_words(&p) / p.N);
+  switch (p.N) {
+    case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft); break;
+    case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft); break;
+    case 1024:
+      if (variant_for(ctx, p) == 4)
+        hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, bsk, npoly, ctx->tw4,
+                           bsk_fft);
+      else if (variant_for(ctx, p) == 3)
+        hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
+      else
+        hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
+      break;
+    case 2048: hipLaunchKernelGGL(k_bsk_to_fft<10>, dim3(npoly), dim3(64), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft); break;
+  }
+}
 static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
   const fhe_params& p = ctx->p;
   hipLaunchKernelGGL(k_ksk_colsum, dim3((p.n + 1 + 255) / 256), dim3(256), 0, st, ctx->ksk, p.k * p.N * p.ks_level,
@@ -294,21 +395,8 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
     hipLaunchKernelGGL(k_ksk_to_i8, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ctx->ksk, K, n1, NB,
                        ctx->ksk8);
   }
-  const int npoly = (int)(fhe_bsk_words(&p) / p.N);
-  switch (p.N) {
-    case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
-    case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
-    case 1024:
-      if (ctx->br_variant == 4)
-        hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw4,
-                           ctx->bsk_fft);
-      else if (ctx->br_variant == 3)
-        hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
-      else
-        hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft);
-      break;
-    case 2048: hipLaunchKernelGGL(k_bsk_to_fft<10>, dim3(npoly), dim3(64), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist, ctx->bsk_fft); break;
-  }
+  bsk_to_fft(ctx, p, ctx->bsk, ctx->bsk_fft, st);
+  if (p.pbs_fast_level) bsk_to_fft(ctx, fast_params(p), ctx->bsk2, ctx->bsk2_fft, st);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -329,7 +417,12 @@ int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream) {
   const int rows_bsk = p.n * (p.k + 1) * p.pbs_level;
   const size_t shm = 8 * (size_t)p.N + p.N;
   hipLaunchKernelGGL(k_keygen_bsk, dim3(rows_bsk), dim3(256), shm, st, K, p.N, p.k, p.pbs_level, p.pbs_base_log,
-                     p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk);
+                     p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk, (uint32_t)TAG_BSK_MASK,
+                     (uint32_t)TAG_BSK_NOISE);
+  if (p.pbs_fast_level)
+    hipLaunchKernelGGL(k_keygen_bsk, dim3(p.n * (p.k + 1) * p.pbs_fast_level), dim3(256), shm, st, K, p.N, p.k,
+                       p.pbs_fast_level, p.pbs_fast_base_log, p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk2,
+                       (uint32_t)TAG_BSK2_MASK, (uint32_t)TAG_BSK2_NOISE);
   hipLaunchKernelGGL(k_keygen_ksk, dim3(big * p.ks_level), dim3(256), 0, st, K, p.n, p.ks_level, p.ks_base_log,
                      p.lwe_noise_bits, ctx->s_small, ctx->s_big, ctx->ksk);
   HIPCHK(ctx, hipGetLastError());
@@ -357,6 +450,17 @@ int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64
   return FHE_OK;
 }
 
+int fhe_export_fast_bsk(fhe_ctx* ctx, uint64_t* h_bsk2) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (!ctx->p.pbs_fast_level) return fail(ctx, FHE_E_STATE, "no fast gadget in these parameters");
+  if (!h_bsk2) return fail(ctx, FHE_E_ARG, "null buffer");
+  const fhe_params q = fast_params(ctx->p);
+  HIPCHK(ctx, hipDeviceSynchronize());
+  HIPCHK(ctx, hipMemcpy(h_bsk2, ctx->bsk2, 8 * fhe_bsk_words(&q), hipMemcpyDeviceToHost));
+  return FHE_OK;
+}
+
 int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
                     const uint64_t* h_ksk) {
   int rc = need_device(ctx);
@@ -369,6 +473,18 @@ int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s
   HIPCHK(ctx, hipMemcpy(ctx->s_big, h_s_big, 8 * (size_t)p.k * p.N, hipMemcpyHostToDevice));
   HIPCHK(ctx, hipMemcpy(ctx->bsk, h_bsk, 8 * fhe_bsk_words(&p), hipMemcpyHostToDevice));
   HIPCHK(ctx, hipMemcpy(ctx->ksk, h_ksk, 8 * fhe_ksk_words(&p), hipMemcpyHostToDevice));
+  if (p.pbs_fast_level) {
+    // the fast-gadget key is not part of the exported set: re-encrypt it
+    // under the imported secrets with fresh randomness
+    ChaKey K;
+    std::random_device rd;
+    for (int i = 0; i < 8; ++i) K.w[i] = rd();
+    const size_t shm = 8 * (size_t)p.N + p.N;
+    hipLaunchKernelGGL(k_keygen_bsk, dim3(p.n * (p.k + 1) * p.pbs_fast_level), dim3(256), shm, nullptr, K, p.N, p.k,
+                       p.pbs_fast_level, p.pbs_fast_base_log, p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk2,
+                       (uint32_t)TAG_BSK2_MASK, (uint32_t)TAG_BSK2_NOISE);
+    HIPCHK(ctx, hipGetLastError());
+  }
   rc = convert_bsk(ctx, nullptr);
   if (rc) return rc;
   HIPCHK(ctx, hipDeviceSynchronize());
@@ -545,24 +661,28 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   return FHE_OK;
 }
 
+// gad = 1: the fast gadget and its key (fhe_params.pbs_fast_*), else the main one
 static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv tv, int mode, uint64_t* out,
-                     uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, hipStream_t st) {
-  const fhe_params& p = ctx->p;
+                     uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, hipStream_t st, int gad = 0) {
+  const bool fast = gad && ctx->p.pbs_fast_level;
+  const fhe_params p = fast ? fast_params(ctx->p) : ctx->p;
+  const c64* bsk_fft = fast ? ctx->bsk2_fft : ctx->bsk_fft;
+  const int var = variant_for(ctx, p);
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_br, st, &e1);
   const dim3 g((unsigned)count), b(64);
 #define BR(LOGM, K)                                                                                           \
   hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
-                     ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
+                     bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
 #define BRV(V, K, W)                                                                                          \
   hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,          \
-                     p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
-#define BR2(K) do { if (ctx->br_variant == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
+                     p.pbs_base_log, bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
+#define BR2(K) do { if (var == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
 #define BR4G(L, A32, D, GG)                                                                                   \
   if (ctx->v4_fl && GG > 1) BR4F(L, A32, D, GG, true); else BR4F(L, A32, D, GG, false)
 #define BR4F(L, A32, D, GG, FLAGS)                                                                             \
   hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),       \
-                     dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, ctx->bsk_fft, ctx->tw4, tv, \
+                     dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, tv, \
                      mode, out, ct_v, refreshed, sign)
 // G = 4 needs 3 waves per SIMD (<= 168 VGPRs): only the 32-bit-accumulator
 // kernels; the u64 ones (208 VGPRs, 2 waves per SIMD) run 2 per workgroup
@@ -579,7 +699,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
     else if (ctx->v4_g == 2) BR4G(2, true, D, 2);    \
     else BR4G(2, true, D, 4);                        \
   } while (0)
-  if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
+  if (p.N == 1024 && p.k == 2 && var == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
       p.pbs_level * p.pbs_base_log <= 31) {
     switch (ctx->v4_dbg) {
       case 1: BR4D(1); break;
@@ -592,7 +712,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       case 128: BR4D(128); break;
       default: BR4D(63); break;
     }
-  } else if (p.N == 1024 && p.k == 2 && ctx->br_variant == 4) {
+  } else if (p.N == 1024 && p.k == 2 && var == 4) {
     const bool a32 = p.pbs_level * p.pbs_base_log <= 31;
     switch (p.pbs_level) {
       case 1: if (a32) BR4(1, true); else BR4(1, false); break;
@@ -696,6 +816,14 @@ int fhe_sign_pbs_count(const fhe_params* params) {
   return 2 * (m / d) + (r >= 3 ? 2 : r) + 1;
 }
 
+int fhe_sign_precise_rounds(const fhe_params* params) {
+  std::string why;
+  if (validate(params, why)) return -1;
+  int d, j;
+  sign_plan(*params, &d, &j);
+  return j;
+}
+
 static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
                         hipStream_t st) {
   const fhe_params& p = ctx->p;
@@ -710,19 +838,23 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
     }
     return FHE_OK;
   }
-  const int d = sign_digits(p), m = P - d;
+  int d, j;
+  sign_plan(p, &d, &j);
+  const int m = P - d;
+  int round = 0;  // bootstraps issued so far; rounds >= j use the fast gadget (sign_plan)
+  auto br = [&](BrTv tv, int mode, uint64_t* sign) -> int {
+    const int gad = round++ >= j;
+    return launch_br(ctx, small, count, tv, mode, nullptr, d_ct_v, nullptr, sign, st, gad);
+  };
   // one c-bit digit at bit b: the pair of rounds on v << (P-b-c) centred by 2^(63-c)
   auto digit = [&](int b, int c) -> int {
     int r;
     // digit MSB (bit b+c-1): sign bootstrap, ct_v -= [bit] * 2^(b+c-1) * Delta
     if ((r = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - c, 1ull << (63 - c), small, st))) return r;
-    if ((r = launch_br(ctx, small, count, BrTv{1ull << (62 - P + b + c), 0, 0}, 1, nullptr, d_ct_v, nullptr,
-                       nullptr, st)))
-      return r;
+    if ((r = br(BrTv{1ull << (62 - P + b + c), 0, 0}, 1, nullptr))) return r;
     // bits [b, b+c-1): top bit is now 0 -> 2^(c-1)-slot staircase, output D' * 2^b * Delta
     if ((r = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - c, 1ull << (63 - c), small, st))) return r;
-    return launch_br(ctx, small, count, BrTv{0, 1ull << (64 - P + b), logN - (c - 1)}, 2, nullptr, d_ct_v,
-                     nullptr, nullptr, st);
+    return br(BrTv{0, 1ull << (64 - P + b), logN - (c - 1)}, 2, nullptr);
   };
   int b = 0;
   for (; b + d <= m; b += d)
@@ -733,13 +865,11 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
   }
   for (; b < m; ++b) {
     if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 1, 1ull << 62, small, st))) return rc;
-    if ((rc = launch_br(ctx, small, count, BrTv{1ull << (63 - P + b), 0, 0}, 1, nullptr, d_ct_v, nullptr, nullptr,
-                        st)))
-      return rc;
+    if ((rc = br(BrTv{1ull << (63 - P + b), 0, 0}, 1, nullptr))) return rc;
   }
   // sign = MSB of the top digit [P-d, P)
   if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, 0, 1ull << (63 - d), small, st))) return rc;
-  return launch_br(ctx, small, count, BrTv{1ull << 62, 0, 0}, 1, nullptr, d_ct_v, nullptr, d_sign, st);
+  return br(BrTv{1ull << 62, 0, 0}, 1, d_sign);
 }
 
 int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, void* stream) {

@@ -15,7 +15,7 @@ __global__ void k_keygen_secrets(ChaKey K, int n, int big, u64* s_small, u64* s_
 // component c_in. body = sum_j A_j * S_j (negacyclic, binary S) + E.
 __global__ void __launch_bounds__(256) k_keygen_bsk(ChaKey K, int N, int k, int L, int beta, int noise_bits,
                                                     const u64* __restrict__ s_small, const u64* __restrict__ s_big,
-                                                    u64* __restrict__ bsk) {
+                                                    u64* __restrict__ bsk, uint32_t tag_mask, uint32_t tag_noise) {
   extern __shared__ u64 shm[];
   u64* A = shm;                                          // N
   unsigned char* S = (unsigned char*)(shm + N);          // N
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) k_keygen_bsk(ChaKey K, int N, int k, int 
     const u64 sid = (u64)row * k + j;
     for (int blk = threadIdx.x; blk < N / 8; blk += 256) {
       u64 w[8];
-      stream_block(K, TAG_BSK_MASK, sid, (uint32_t)blk, w);
+      stream_block(K, tag_mask, sid, (uint32_t)blk, w);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         A[8 * blk + q] = w[q];
@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(256) k_keygen_bsk(ChaKey K, int N, int k, int 
   }
   for (int q = 0; q < per; ++q) {
     const int t = threadIdx.x + 256 * q;
-    u64 b = body[q] + (u64)tuniform(stream_word(K, TAG_BSK_NOISE, (u64)row, (u64)t), noise_bits);
+    u64 b = body[q] + (u64)tuniform(stream_word(K, tag_noise, (u64)row, (u64)t), noise_bits);
     dst[(size_t)k * N + t] = b;
   }
   __syncthreads();

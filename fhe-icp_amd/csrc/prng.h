@@ -21,6 +21,8 @@ enum StreamTag : uint32_t {
   TAG_KSK_NOISE = 6,
   TAG_ENC_MASK = 7,
   TAG_ENC_NOISE = 8,
+  TAG_BSK2_MASK = 9,   // the fast-gadget bootstrapping key (fhe_params.pbs_fast_*)
+  TAG_BSK2_NOISE = 10,
 };
 
 struct ChaKey {

@@ -15,7 +15,10 @@ FHE_OK = 0
 ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOMEM"}
 
 PARAM_FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
-                "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits")
+                "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
+                "pbs_fast_base_log", "pbs_fast_level")
+# fields a caller may leave out (0 = auto / none)
+OPTIONAL_FIELDS = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level")
 
 
 class FheParams(C.Structure):
@@ -43,6 +46,7 @@ SIGNATURES = [
     ("fhe_keygen_key", C.c_int, [_CTXP, C.POINTER(C.c_uint32), _vp]),
     ("fhe_export_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
     ("fhe_import_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
+    ("fhe_export_fast_bsk", C.c_int, [_CTXP, _vp]),
     ("fhe_encrypt_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _vp, _vp]),
     ("fhe_decrypt_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_decrypt_bits_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
@@ -54,6 +58,7 @@ SIGNATURES = [
     ("fhe_sign_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_sign_digit_bits", C.c_int, [_P]),
     ("fhe_sign_pbs_count", C.c_int, [_P]),
+    ("fhe_sign_precise_rounds", C.c_int, [_P]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     ("fhe_encrypt_seeded_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
@@ -107,4 +112,4 @@ def check(rc: int, ctx=None) -> None:
 
 
 def params_struct(d: dict) -> FheParams:
-    return FheParams(**{f: int(d.get(f, 0) if f == "sign_digit_bits" else d[f]) for f in PARAM_FIELDS})
+    return FheParams(**{f: int(d.get(f, 0) if f in OPTIONAL_FIELDS else d[f]) for f in PARAM_FIELDS})

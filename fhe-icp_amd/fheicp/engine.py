@@ -86,6 +86,17 @@ class Engine:
                                                        for k in ("s_small", "s_big", "bsk", "ksk"))))
         return out
 
+    def export_fast_bsk(self) -> np.ndarray:
+        """The fast gadget's bootstrapping key (params.pbs_fast_*)."""
+        p = self.params
+        if not p.pbs_fast_level:
+            raise ValueError("these parameters have no fast gadget")
+        q = _lib.params_struct({**p.as_dict(), "pbs_base_log": p.pbs_fast_base_log,
+                                "pbs_level": p.pbs_fast_level})
+        out = np.zeros(self._L.fhe_bsk_words(C.byref(q)), np.uint64)
+        self._chk(self._L.fhe_export_fast_bsk(self._ctx, C.c_void_p(out.ctypes.data)))
+        return out
+
     def import_keys(self, keys: dict) -> None:
         arrs = [np.ascontiguousarray(keys[k], dtype=np.uint64) for k in ("s_small", "s_big", "bsk", "ksk")]
         self._chk(self._L.fhe_import_keys(self._ctx, *(C.c_void_p(a.ctypes.data) for a in arrs)))

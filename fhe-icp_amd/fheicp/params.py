@@ -32,6 +32,11 @@ class SchemeParams:
     # digit width of the sign extraction; 0 = sign_digit_bits(): the widest
     # meeting the noise bar (fhe_params.sign_digit_bits)
     sign_digit_bits: int = 0
+    # second, faster bootstrap gadget (same keys, its own bootstrapping key)
+    # for the sign-extraction rounds whose noise is not amplified much; 0, 0 =
+    # none (fhe_params.pbs_fast_base_log / pbs_fast_level, sign_plan())
+    pbs_fast_base_log: int = 0
+    pbs_fast_level: int = 0
 
     def as_dict(self) -> dict:
         return asdict(self)
@@ -49,23 +54,77 @@ class SchemeParams:
 # (sign_digit_bits) are used where they too keep 9.2 sigma.
 PBS_GADGETS = ((17, 15, 2), (21, 12, 3), (23, 10, 4), (25, 8, 5), (26, 7, 6), (27, 6, 7))
 SIGMA_BAR = 9.2
+FAST_GADGET = (15, 2)
+
+
+def sign_rounds(P: int, d: int):
+    """The bootstraps of fhe_sign_batch in order as (shift, log2 margin): the
+    round decides on v << shift, so every earlier bootstrap's output noise is
+    amplified by 2^shift (fheicp.hip sign_rounds)."""
+    out, b, m = [], 0, P - d
+    while b + d <= m:
+        out += [(P - b - d, -(d + 1))] * 2
+        b += d
+    if m - b >= 3:
+        c = m - b
+        out += [(P - b - c, -(c + 1))] * 2
+        b = m
+    while b < m:
+        out.append((P - b - 1, -2))
+        b += 1
+    out.append((0, -(d + 1)))
+    return out
+
+
+def _plan_worst(p: "SchemeParams", d: int, j: int) -> float:
+    """Worst decision margin (sigmas) when the first j bootstraps use the main
+    gadget and the rest the fast one."""
+    v_main = _variances(p)[0]
+    v_fast = _variances(replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level))[0]
+    _, v_ks, v_ms = _variances(p)
+    acc, worst = 0.0, math.inf
+    for r, (sh, ml) in enumerate(sign_rounds(p.msg_bits, d)):
+        worst = min(worst, 2.0 ** ml / math.sqrt(acc * 4.0 ** sh + v_ks + v_ms))
+        acc += v_main if r < j else v_fast
+    return worst
+
+
+def sign_plan(p: "SchemeParams"):
+    """(d, j) of fhe_sign_batch: digit width d and how many leading bootstraps
+    use the main gadget (the rest use the fast one). Without a fast gadget: d =
+    the explicit p.sign_digit_bits, else 4 if its worst round keeps SIGMA_BAR
+    sigmas, else 3, and every round on the main gadget. With one: the widest d
+    (or the explicit one) and the fewest main-gadget rounds that keep every
+    round at SIGMA_BAR. (0, P) when P < 4 (single-bit rounds)."""
+    P = p.msg_bits
+    if P < 4:
+        return 0, P
+    if p.sign_digit_bits not in (0, 3, 4):
+        raise ValueError("sign_digit_bits must be 0 (auto), 3 or 4")
+    if not p.pbs_fast_level:
+        if p.sign_digit_bits:
+            d = min(p.sign_digit_bits, P)
+        else:
+            d = min(4, P) if _digit_margin(p, min(4, P)) >= SIGMA_BAR else 3
+        return d, len(sign_rounds(P, d))
+    first = min(p.sign_digit_bits, P) if p.sign_digit_bits else min(4, P)
+    last = first if p.sign_digit_bits else 3
+    for d in range(first, last - 1, -1):
+        R = len(sign_rounds(P, d))
+        for j in range(R + 1):
+            if _plan_worst(p, d, j) >= SIGMA_BAR:
+                return d, j
+    return last, len(sign_rounds(P, last))
 
 
 def sign_digit_bits(p: "SchemeParams") -> int:
-    """Digit width of fhe_sign_batch (fhe_sign_digit_bits): the explicit
-    p.sign_digit_bits (3 or 4), else 4 if its worst round keeps SIGMA_BAR
-    sigmas (noise_report), else 3; 0 when P < 4 (single-bit rounds)."""
-    P = p.msg_bits
-    if P < 4:
-        return 0
-    if p.sign_digit_bits not in (0, 3, 4):
-        raise ValueError("sign_digit_bits must be 0 (auto), 3 or 4")
-    if p.sign_digit_bits:
-        return min(p.sign_digit_bits, P)
-    for d in range(min(4, P), 3, -1):
-        if _digit_margin(p, d) >= SIGMA_BAR:
-            return d
-    return 3
+    """Digit width of fhe_sign_batch (fhe_sign_digit_bits), from sign_plan."""
+    return sign_plan(p)[0]
+
+
+def sign_precise_rounds(p: "SchemeParams") -> int:
+    """Bootstraps of fhe_sign_batch on the main gadget (fhe_sign_precise_rounds)."""
+    return sign_plan(p)[1]
 
 
 def sign_pbs_count(p) -> int:
@@ -82,10 +141,19 @@ def sign_pbs_count(p) -> int:
     return 2 * (m // d) + (2 if r >= 3 else r) + 1
 
 
-def params_for_bits(P: int) -> SchemeParams:
+def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
+    """The gadget of PBS_GADGETS for width P; with fast, P > 17 also gets the
+    (15, 2) gadget for the sign rounds that do not need the precise one, if
+    the plan puts at least one round on it."""
     for pmax, beta, lvl in PBS_GADGETS:
         if P <= pmax:
-            return SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
+            p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
+            if fast and (beta, lvl) != FAST_GADGET:
+                q = replace(p, pbs_fast_base_log=FAST_GADGET[0], pbs_fast_level=FAST_GADGET[1])
+                d, j = sign_plan(q)
+                if j < len(sign_rounds(P, d)):
+                    p = q
+            return p
     raise ValueError(f"accumulator width P={P} exceeds the supported 27 bits")
 
 
@@ -129,7 +197,8 @@ def noise_report(p: SchemeParams, method: str = "digits") -> dict:
     bit 0 amplified by 2^(P-2), decision margin 1/4 of the torus.
     method "digits" (fhe_sign_batch, P >= 4) with d = sign_digit_bits(p): the
     staircase bootstrap of the first d-bit digit, the digit-MSB bootstrap's
-    noise amplified by 2^(P-d), margin 2^-(d+1).
+    noise amplified by 2^(P-d), margin 2^-(d+1); with a fast
+    gadget, the worst round of sign_plan's main/fast schedule.
     """
     if method not in ("bits", "digits"):
         raise ValueError(method)
@@ -139,6 +208,10 @@ def noise_report(p: SchemeParams, method: str = "digits") -> dict:
     v_total = v_amp + v_ks + v_ms
     sigma = math.sqrt(v_total)
     margin_sigmas = (2.0 ** -(d + 1) if d > 1 else 0.25) / sigma
+    if d > 1 and p.pbs_fast_level:
+        # two gadgets: the worst round of sign_plan's schedule
+        margin_sigmas = _plan_worst(p, d, sign_plan(p)[1])
+        sigma = 2.0 ** -(d + 1) / margin_sigmas
     return {
         "digit_bits": d if d > 1 else 1,
         "log2_sigma_pbs": 0.5 * math.log2(v_pbs),

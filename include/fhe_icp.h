@@ -58,6 +58,12 @@ typedef struct fhe_params {
   int32_t sign_digit_bits; /* digit width d of fhe_sign_batch (3 or 4), or 0: the
                               widest d whose worst round keeps >= 9.2 sigma
                               (fhe_sign_digit_bits) */
+  int32_t pbs_fast_base_log; /* optional second bootstrap gadget (0, 0: none). The */
+  int32_t pbs_fast_level;    /* sign extraction runs its first fhe_sign_precise_rounds
+                                bootstraps on (pbs_base_log, pbs_level) and the rest on
+                                this cheaper one. keygen makes a second
+                                bootstrapping key for it (fhe_export_fast_bsk); import
+                                re-encrypts it with fresh randomness. */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;
@@ -93,6 +99,10 @@ int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream);
 int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64_t* h_bsk, uint64_t* h_ksk);
 int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
                     const uint64_t* h_ksk);
+/* the fast gadget's bootstrapping key (same layout as bsk, fhe_bsk_words of
+ * the params with pbs_base_log/pbs_level replaced by the fast pair; stream
+ * tags 9/10). FHE_E_STATE without a fast gadget. Synchronous. */
+int fhe_export_fast_bsk(fhe_ctx* ctx, uint64_t* h_bsk2);
 
 /* ---- client side: encrypt / decrypt --------------------------------------
  * Replaces the per-sample encrypt/decrypt of predict(fhe="execute")
@@ -138,6 +148,9 @@ int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_si
  * when it is 0); 0 for msg_bits < 4 (single-bit rounds); -1 on bad params. */
 int fhe_sign_digit_bits(const fhe_params* params);
 int fhe_sign_pbs_count(const fhe_params* params);
+/* how many of them (the first ones) run on the main gadget; all of them
+ * without a fast gadget */
+int fhe_sign_precise_rounds(const fhe_params* params);
 /* Bootstrap with a staircase test vector over 2^log_slots slots of the half
  * torus: output phase ~ base + floor(phase * 2^log_slots / 2^63) * step for an
  * input phase in [0, 2^63) (negacyclic beyond). log_slots = 0, step = 0 is

@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
-          "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits")
+          "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
+          "pbs_fast_base_log", "pbs_fast_level")
 
 
 class fhe_params(C.Structure):
@@ -49,7 +50,7 @@ class GpuCompare:
         for name, (res, args) in _PROTOS.items():
             getattr(L, name).restype = res
             getattr(L, name).argtypes = args
-        self.P = fhe_params(**{f: int(params[f]) for f in FIELDS})
+        self.P = fhe_params(**{f: int(params.get(f, 0)) for f in FIELDS})
         self.ctx = _vp()
         self._ok(L.fhe_ctx_create(C.byref(self.P), device, C.byref(self.ctx)))
         self._ok(L.fhe_keygen(self.ctx, key_seed, None))

@@ -45,6 +45,8 @@ typedef struct {
   int32_t glwe_noise_bits; /* TUniform bound: GLWE / BSK / big-key LWE */
   int32_t msg_bits;        /* P: message width */
   int32_t sign_digit_bits; /* sign-extraction digit width, 0 = noise-model choice */
+  int32_t pbs_fast_base_log; /* second (fast) bootstrap gadget for the low-  */
+  int32_t pbs_fast_level;    /* amplification sign rounds; 0, 0 = none      */
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -123,7 +125,7 @@ static int64_t tuniform(uint64_t w, int b) {
 int64_t ref_tuniform(uint64_t w, int b) { return tuniform(w, b); }
 
 enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, TAG_KSK_MASK = 5,
-       TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8 };
+       TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10 };
 
 /* --------------------------------------------------- negacyclic product --- */
 /* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
@@ -171,19 +173,12 @@ size_t ref_bsk_words(const ref_params* P) { return (size_t)P->n * rows(P) * (P->
 size_t ref_ksk_words(const ref_params* P) { return (size_t)P->k * P->N * P->ks_level * (P->n + 1); }
 
 /* --------------------------------------------------------------- keygen --- */
-/* s_small[n] (0/1), s_big[kN] (0/1), bsk[ref_bsk_words], ksk[ref_ksk_words] */
-int ref_keygen(const ref_params* P, uint64_t seed, uint64_t* s_small, uint64_t* s_big, uint64_t* bsk,
-               uint64_t* ksk) {
-  ref_key K;
-  key_from_seed(seed, &K);
-  const int n = P->n, k = P->k, N = P->N, L = P->pbs_level, R = rows(P);
-  ref_stream st;
-  stream_init(&st, &K, TAG_SK_SMALL, 0);
-  for (int i = 0; i < n; ++i) s_small[i] = stream_word(&st, (uint64_t)i) & 1;
-  stream_init(&st, &K, TAG_SK_GLWE, 0);
-  for (int i = 0; i < k * N; ++i) s_big[i] = stream_word(&st, (uint64_t)i) & 1;
-
-  /* BSK rows: GLWE_S(0) + s_small[i] * g_lvl on component c_in, g_lvl = 2^(64 - lvl*beta) */
+/* BSK rows: GLWE_S(0) + s_small[i] * g_lvl on component c_in, g_lvl = 2^(64 - lvl*beta);
+ * (beta, L) and the stream tags select the main or the fast gadget's key */
+static void bsk_gen(const ref_params* P, const ref_key* Kp, int beta, int L, int tag_mask, int tag_noise,
+                    const uint64_t* s_small, const uint64_t* s_big, uint64_t* bsk) {
+  const ref_key K = *Kp;
+  const int n = P->n, k = P->k, N = P->N, R = (k + 1) * L;
 #pragma omp parallel for schedule(dynamic)
   for (int i = 0; i < n; ++i) {
     uint64_t* scratch = (uint64_t*)malloc(8 * (size_t)(16 * N));
@@ -196,18 +191,47 @@ int ref_keygen(const ref_params* P, uint64_t seed, uint64_t* s_small, uint64_t* 
       for (int t = 0; t < N; ++t) body[t] = 0;
       for (int j = 0; j < k; ++j) {
         uint64_t* A = row + (size_t)j * N;
-        stream_init(&sm, &K, TAG_BSK_MASK, ((uint64_t)i * R + r) * k + j);
+        stream_init(&sm, &K, tag_mask, ((uint64_t)i * R + r) * k + j);
         for (int t = 0; t < N; ++t) A[t] = stream_word(&sm, (uint64_t)t);
         for (int t = 0; t < N; ++t) S[t] = s_big[j * N + t];
         negacyclic_mac(A, S, body, N, scratch);
       }
-      stream_init(&sn, &K, TAG_BSK_NOISE, (uint64_t)i * R + r);
+      stream_init(&sn, &K, tag_noise, (uint64_t)i * R + r);
       for (int t = 0; t < N; ++t) body[t] += (uint64_t)tuniform(stream_word(&sn, (uint64_t)t), P->glwe_noise_bits);
-      if (s_small[i]) row[(size_t)c_in * N] += ((uint64_t)1) << (64 - lvl * P->pbs_base_log);
+      if (s_small[i]) row[(size_t)c_in * N] += ((uint64_t)1) << (64 - lvl * beta);
     }
     free(scratch);
     free(S);
   }
+}
+
+/* the fast gadget's bootstrapping key (fhe_keygen with pbs_fast_*): same
+ * secrets, TAG_BSK2_* streams; bsk2 has ref_bsk_words of the fast gadget */
+size_t ref_bsk2_words(const ref_params* P) {
+  return (size_t)P->n * (P->k + 1) * P->pbs_fast_level * (P->k + 1) * P->N;
+}
+int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, const uint64_t* s_small, const uint64_t* s_big,
+                        uint64_t* bsk2) {
+  if (!P->pbs_fast_level) return -1;
+  ref_key K;
+  key_from_seed(seed, &K);
+  bsk_gen(P, &K, P->pbs_fast_base_log, P->pbs_fast_level, TAG_BSK2_MASK, TAG_BSK2_NOISE, s_small, s_big, bsk2);
+  return 0;
+}
+
+/* s_small[n] (0/1), s_big[kN] (0/1), bsk[ref_bsk_words], ksk[ref_ksk_words] */
+int ref_keygen(const ref_params* P, uint64_t seed, uint64_t* s_small, uint64_t* s_big, uint64_t* bsk,
+               uint64_t* ksk) {
+  ref_key K;
+  key_from_seed(seed, &K);
+  const int n = P->n, k = P->k, N = P->N;
+  ref_stream st;
+  stream_init(&st, &K, TAG_SK_SMALL, 0);
+  for (int i = 0; i < n; ++i) s_small[i] = stream_word(&st, (uint64_t)i) & 1;
+  stream_init(&st, &K, TAG_SK_GLWE, 0);
+  for (int i = 0; i < k * N; ++i) s_big[i] = stream_word(&st, (uint64_t)i) & 1;
+
+  bsk_gen(P, &K, P->pbs_base_log, P->pbs_level, TAG_BSK_MASK, TAG_BSK_NOISE, s_small, s_big, bsk);
 
   /* key-switching key big -> small */
   const int KL = P->ks_level;
@@ -537,40 +561,120 @@ static void sign_round(const ref_params* P, const uint64_t* bsk, const uint64_t*
   for (int t = 0; t < Wb; ++t) cv[t] -= ob[t];
 }
 
-/* Digit width of the sign extraction: the explicit
- * sign_digit_bits, else d = 4 if its worst round -- margin
- * 2^-(d+1), the previous bootstrap's variance amplified by 4^(P-d), plus the
- * key-switch and modulus-switch variances -- keeps >= 9.2 sigma, else 3. */
+/* Plan of the sign extraction: digit width d and the number
+ * j of leading bootstraps on the main gadget (the rest on the fast one).
+ * Round r decides on v << shift_r with margin 2^mlog_r; every earlier
+ * bootstrap's output variance is amplified by 4^shift_r, the key-switch and
+ * modulus-switch variances are not. Without a fast gadget: the explicit
+ * sign_digit_bits, else d = 4 if its worst round keeps >= 9.2 sigma, else 3;
+ * j = all rounds. With one: the widest d (or the explicit one) and the fewest
+ * main rounds keeping every round at 9.2 sigma. */
 static double tu_var(int b) { return (ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
 
-static int digit_bits(const ref_params* P) {
-  if (P->msg_bits < 4) return 0;
-  if (P->sign_digit_bits) return P->sign_digit_bits < P->msg_bits ? P->sign_digit_bits : P->msg_bits;
-  const double q2 = ldexp(1.0, 128);
-  const double beta = ldexp(1.0, P->pbs_base_log), bk = ldexp(1.0, P->ks_base_log);
-  const double key = (double)P->n * P->pbs_level * (P->k + 1) * P->N * (beta * beta + 2) / 12.0 *
-                     tu_var(P->glwe_noise_bits) / q2;
-  const double rnd = (double)P->n * (1 + P->k * P->N / 2.0) / (12.0 * pow(beta, 2.0 * P->pbs_level));
-  const double ks = (double)P->k * P->N * P->ks_level * (bk * bk + 2) / 12.0 * tu_var(P->lwe_noise_bits) / q2 +
+static double pbs_variance(const ref_params* P, int base_log, int L) {
+  const double beta = ldexp(1.0, base_log);
+  const double key = (double)P->n * L * (P->k + 1) * P->N * (beta * beta + 2) / 12.0 * tu_var(P->glwe_noise_bits) /
+                     ldexp(1.0, 128);
+  return key + (double)P->n * (1 + P->k * P->N / 2.0) / (12.0 * pow(beta, 2.0 * L));
+}
+static double fixed_variance(const ref_params* P) {
+  const double bk = ldexp(1.0, P->ks_base_log);
+  const double ks = (double)P->k * P->N * P->ks_level * (bk * bk + 2) / 12.0 * tu_var(P->lwe_noise_bits) /
+                        ldexp(1.0, 128) +
                     P->k * P->N / 2.0 * ldexp(1.0, -2 * P->ks_level * P->ks_base_log) / 12.0;
-  const double ms = (P->n / 2.0 + 1) / 12.0 / ((2.0 * P->N) * (2.0 * P->N));
-  for (int d = P->msg_bits < 4 ? P->msg_bits : 4; d > 3; --d) {
-    const double sigma = sqrt((key + rnd) * ldexp(1.0, 2 * (P->msg_bits - d)) + ks + ms);
-    if (ldexp(1.0, -(d + 1)) / sigma >= 9.2) return d;
+  return ks + (P->n / 2.0 + 1) / 12.0 / ((2.0 * P->N) * (2.0 * P->N));
+}
+/* rounds of the extraction in order: (shift, log2 margin); returns the count */
+static int plan_rounds(int Pb, int d, int* shift, int* mlog) {
+  int R = 0, b = 0;
+  const int m = Pb - d;
+  for (; b + d <= m; b += d)
+    for (int t = 0; t < 2; ++t) { shift[R] = Pb - b - d; mlog[R++] = -(d + 1); }
+  if (m - b >= 3) {
+    const int c = m - b;
+    for (int t = 0; t < 2; ++t) { shift[R] = Pb - b - c; mlog[R++] = -(c + 1); }
+    b = m;
   }
-  return 3;
+  for (; b < m; ++b) { shift[R] = Pb - b - 1; mlog[R++] = -2; }
+  shift[R] = 0; mlog[R++] = -(d + 1);
+  return R;
+}
+static double plan_margin(const ref_params* P, int d, int j) {
+  int sh[64], ml[64];
+  const int R = plan_rounds(P->msg_bits, d, sh, ml);
+  const double vm = pbs_variance(P, P->pbs_base_log, P->pbs_level);
+  const double vf = P->pbs_fast_level ? pbs_variance(P, P->pbs_fast_base_log, P->pbs_fast_level) : vm;
+  const double fx = fixed_variance(P);
+  double acc = 0, worst = INFINITY;
+  for (int r = 0; r < R; ++r) {
+    const double m = ldexp(1.0, ml[r]) / sqrt(acc * ldexp(1.0, 2 * sh[r]) + fx);
+    if (m < worst) worst = m;
+    acc += r < j ? vm : vf;
+  }
+  return worst;
+}
+static void sign_plan(const ref_params* P, int* d_out, int* j_out) {
+  int sh[64], ml[64];
+  const int Pb = P->msg_bits, d4 = Pb < 4 ? Pb : 4;
+  if (Pb < 4) { *d_out = 0; *j_out = Pb; return; }
+  if (!P->pbs_fast_level) {
+    int d = 3;
+    if (P->sign_digit_bits) {
+      d = P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb;
+    } else {
+      /* the worst round of a single-gadget plan: the staircase round of the
+       * lowest digit, the preceding bootstrap amplified by 4^(P-d) */
+      const double v = pbs_variance(P, P->pbs_base_log, P->pbs_level) * ldexp(1.0, 2 * (Pb - d4)) +
+                       fixed_variance(P);
+      if (ldexp(1.0, -(d4 + 1)) / sqrt(v) >= 9.2) d = d4;
+    }
+    *d_out = d;
+    *j_out = plan_rounds(Pb, d, sh, ml);
+    return;
+  }
+  const int first = P->sign_digit_bits ? (P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb) : d4;
+  const int last = P->sign_digit_bits ? first : 3;
+  for (int d = first; d >= last; --d) {
+    const int R = plan_rounds(Pb, d, sh, ml);
+    for (int j = 0; j <= R; ++j)
+      if (plan_margin(P, d, j) >= 9.2) { *d_out = d; *j_out = j; return; }
+  }
+  *d_out = last;
+  *j_out = plan_rounds(Pb, last, sh, ml);
+}
+static int digit_bits(const ref_params* P) {
+  int d, j;
+  sign_plan(P, &d, &j);
+  return d;
+}
+
+/* the bootstrap gadget and key of round r: the main one for r < j, else the fast one */
+typedef struct {
+  const ref_params* P;
+  ref_params Pf; /* P seen through the fast gadget */
+  const uint64_t *bsk, *bsk2;
+  int j, r;
+} gadget_sched;
+static void sched_next(gadget_sched* g, const ref_params** Pr, const uint64_t** bk) {
+  const int fast = g->bsk2 && g->r++ >= g->j;
+  *Pr = fast ? &g->Pf : g->P;
+  *bk = fast ? g->bsk2 : g->bsk;
 }
 
 /* One c-bit digit [b, b+c) of the value in cv: a sign bootstrap of its top bit
  * (v << (P-b-c), centred by 2^(63-c), tv 2^(62-P+b+c)), then a
  * 2^(c-1)-slot staircase of its c-1 low bits (step 2^(64-P+b)). */
-static void digit_rounds(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* cv, int b, int c,
-                         uint64_t* sh, uint64_t* sm, uint64_t* ob, uint64_t* work) {
-  const int Pb = P->msg_bits, lgN = ilog2(P->N);
+static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int b, int c, uint64_t* sh, uint64_t* sm,
+                         uint64_t* ob, uint64_t* work) {
+  const ref_params* Pr;
+  const uint64_t* bk;
+  const int Pb = g->P->msg_bits, lgN = ilog2(g->P->N);
   const tv_desc hi = {1ull << (62 - Pb + b + c), 0, 0};
-  sign_round(P, bsk, ksk, cv, Pb - b - c, 1ull << (63 - c), &hi, 1, sh, sm, ob, work);
+  sched_next(g, &Pr, &bk);
+  sign_round(Pr, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &hi, 1, sh, sm, ob, work);
   const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - (c - 1)};
-  sign_round(P, bsk, ksk, cv, Pb - b - c, 1ull << (63 - c), &lo, 2, sh, sm, ob, work);
+  sched_next(g, &Pr, &bk);
+  sign_round(Pr, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &lo, 2, sh, sm, ob, work);
 }
 
 /* Sign of the P-bit value in ct_v with d-bit digits (the
@@ -578,19 +682,32 @@ static void digit_rounds(const ref_params* P, const uint64_t* bsk, const uint64_
  * digits [b, b+d) by digit_rounds, a leftover of >= 3 bits as one shorter
  * digit, of 1-2 bits by single-bit rounds; then the sign of the top d bits
  * (centred by 2^(63-d), tv 2^62). sign[count x (kN+1)] encrypts [v < 0] at
- * 2^63; ct_v is consumed. */
-void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
-                      uint64_t* sign) {
-  const int Wb = P->k * P->N + 1, Pb = P->msg_bits, d = digit_bits(P);
+ * 2^63; ct_v is consumed. With a fast gadget (P->pbs_fast_*) and its key bsk2,
+ * bootstraps from the j-th on (sign_plan) use it; bsk2 = NULL plans as if no
+ * fast gadget were set. */
+void ref_sign_extract2(const ref_params* P0, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* ksk,
+                       uint64_t* ct_v, int64_t count, uint64_t* sign) {
+  ref_params Pm = *P0;
+  if (!bsk2) Pm.pbs_fast_base_log = Pm.pbs_fast_level = 0;
+  const ref_params* P = &Pm;
+  const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
+  int d, j;
+  sign_plan(P, &d, &j);
+  ref_params Pf = *P;
+  if (P->pbs_fast_level) { Pf.pbs_base_log = P->pbs_fast_base_log; Pf.pbs_level = P->pbs_fast_level; }
+  const size_t ww = pbs_work_words(P) > pbs_work_words(&Pf) ? pbs_work_words(P) : pbs_work_words(&Pf);
 #pragma omp parallel
   {
-    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+    uint64_t* work = (uint64_t*)malloc(8 * ww);
     uint64_t* sh = (uint64_t*)malloc(8 * (size_t)Wb);
     uint64_t* sm = (uint64_t*)malloc(8 * (size_t)(P->n + 1));
     uint64_t* ob = (uint64_t*)malloc(8 * (size_t)Wb);
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c) {
       uint64_t* cv = ct_v + (size_t)c * Wb;
+      gadget_sched g = {P, Pf, bsk, P->pbs_fast_level ? bsk2 : NULL, j, 0};
+      const ref_params* Pr;
+      const uint64_t* bk;
       if (Pb < 4) {
         for (int i = 0; i < Pb; ++i) {
           const tv_desc t = {1ull << (63 - Pb + i), 0, 0};
@@ -599,22 +716,34 @@ void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* 
       } else {
         const int m = Pb - d;
         int b = 0;
-        for (; b + d <= m; b += d) digit_rounds(P, bsk, ksk, cv, b, d, sh, sm, ob, work);
+        for (; b + d <= m; b += d) digit_rounds(&g, ksk, cv, b, d, sh, sm, ob, work);
         if (m - b >= 3) {
-          digit_rounds(P, bsk, ksk, cv, b, m - b, sh, sm, ob, work);
+          digit_rounds(&g, ksk, cv, b, m - b, sh, sm, ob, work);
           b = m;
         }
         for (; b < m; ++b) {
           const tv_desc t = {1ull << (63 - Pb + b), 0, 0};
-          sign_round(P, bsk, ksk, cv, Pb - b - 1, 1ull << 62, &t, 1, sh, sm, ob, work);
+          sched_next(&g, &Pr, &bk);
+          sign_round(Pr, bk, ksk, cv, Pb - b - 1, 1ull << 62, &t, 1, sh, sm, ob, work);
         }
         const tv_desc top = {1ull << 62, 0, 0};
-        sign_round(P, bsk, ksk, cv, 0, 1ull << (63 - d), &top, 1, sh, sm, ob, work);
+        sched_next(&g, &Pr, &bk);
+        sign_round(Pr, bk, ksk, cv, 0, 1ull << (63 - d), &top, 1, sh, sm, ob, work);
       }
       memcpy(sign + (size_t)c * Wb, ob, 8 * (size_t)Wb);
     }
     free(work); free(sh); free(sm); free(ob);
   }
+}
+void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
+                      uint64_t* sign) {
+  ref_sign_extract2(P, bsk, NULL, ksk, ct_v, count, sign);
+}
+
+int ref_sign_precise_rounds(const ref_params* P) {
+  int d, j;
+  sign_plan(P, &d, &j);
+  return j;
 }
 
 int ref_sign_digit_bits(const ref_params* P) { return digit_bits(P); }

@@ -16,7 +16,9 @@ _HERE = Path(__file__).resolve().parent
 _LIB_PATH = _HERE / "build" / "libtfhe_ref.so"
 
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
-          "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits")
+          "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
+          "pbs_fast_base_log", "pbs_fast_level")
+OPTIONAL = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level")
 
 
 class RefParams(C.Structure):
@@ -57,6 +59,10 @@ def lib():
         L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
         L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_extract2.argtypes = [P, u64p, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_precise_rounds.argtypes = [P]; L.ref_sign_precise_rounds.restype = C.c_int
+        L.ref_bsk2_words.argtypes = [P]; L.ref_bsk2_words.restype = C.c_size_t
+        L.ref_keygen_fast_bsk.argtypes = [P, C.c_uint64, u64p, u64p, u64p]
         L.ref_sign_pbs_count.argtypes = [P]; L.ref_sign_pbs_count.restype = C.c_int
         L.ref_sign_digit_bits.argtypes = [P]; L.ref_sign_digit_bits.restype = C.c_int
         L.ref_negacyclic_mul.argtypes = [u64p, u64p, u64p, C.c_int]
@@ -87,7 +93,7 @@ class RefTFHE:
     """Exact CPU TFHE with the same parameters and PRNG streams as the GPU."""
 
     def __init__(self, params: dict, seed: int):
-        self.params = {f: int(params.get(f, 0) if f == "sign_digit_bits" else params[f]) for f in FIELDS}
+        self.params = {f: int(params.get(f, 0) if f in OPTIONAL else params[f]) for f in FIELDS}
         self.P = RefParams(**self.params)
         L = lib()
         self.n, self.k, self.N = self.params["n"], self.params["k"], self.params["N"]
@@ -98,6 +104,12 @@ class RefTFHE:
         self.ksk = np.zeros(L.ref_ksk_words(C.byref(self.P)), np.uint64)
         L.ref_keygen(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big), u64(self.bsk),
                      u64(self.ksk))
+        # the fast gadget's bootstrapping key (fhe_keygen generates it too)
+        self.bsk2 = None
+        if self.params["pbs_fast_level"]:
+            self.bsk2 = np.zeros(L.ref_bsk2_words(C.byref(self.P)), np.uint64)
+            L.ref_keygen_fast_bsk(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big),
+                                  u64(self.bsk2))
 
     def with_msg_bits(self, P: int) -> "RefTFHE":
         self.params["msg_bits"] = int(P)
@@ -201,7 +213,8 @@ class RefTFHE:
         cv = np.array(ct_v, dtype=np.uint64, copy=True, order="C")
         cnt = cv.size // (self.big + 1)
         sign = np.zeros((cnt, self.big + 1), np.uint64)
-        lib().ref_sign_extract(C.byref(self.P), u64(self.bsk), u64(self.ksk), u64(cv), cnt, u64(sign))
+        bsk2 = u64(self.bsk2) if self.bsk2 is not None else None
+        lib().ref_sign_extract2(C.byref(self.P), u64(self.bsk), bsk2, u64(self.ksk), u64(cv), cnt, u64(sign))
         return sign
 
     def bit_extract(self, ct_v: np.ndarray):
@@ -246,7 +259,7 @@ def key_from_seed(seed: int) -> np.ndarray:
 
 
 def _ref_params(params: dict) -> RefParams:
-    return RefParams(**{f: int(params.get(f, 0) if f == "sign_digit_bits" else params[f]) for f in FIELDS})
+    return RefParams(**{f: int(params.get(f, 0) if f in OPTIONAL else params[f]) for f in FIELDS})
 
 
 def sign_digit_bits(params: dict) -> int:
@@ -255,3 +268,7 @@ def sign_digit_bits(params: dict) -> int:
 
 def sign_pbs_count(params: dict) -> int:
     return int(lib().ref_sign_pbs_count(C.byref(_ref_params(params))))
+
+
+def sign_precise_rounds(params: dict) -> int:
+    return int(lib().ref_sign_precise_rounds(C.byref(_ref_params(params))))

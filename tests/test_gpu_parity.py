@@ -212,11 +212,62 @@ def test_sign_toy_all_values_vs_oracle(need_gpu, oracle_lib, P, dbits):
     eng.close()
 
 
-@pytest.mark.parametrize("P,dbits", [(16, 0), (16, 3), (21, 0)])
-def test_sign_real_params(need_gpu, P, dbits):
+TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_level=2)
+
+
+@pytest.mark.parametrize("P", [8, 19])
+def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P):
+    """Both bootstrapping keys of a two-gadget parameter set (toy (12,3)+(8,2);
+    real P=19: (12,3)+(15,2)) are bit-exact against the oracle's keygen."""
+    prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 17 else params_for_bits(P)
+    assert prm.pbs_fast_level
+    eng = Engine(prm, 0)
+    eng.keygen(4321)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 4321)
+    assert np.array_equal(eng.export_keys()["bsk"], ref.bsk)
+    assert np.array_equal(eng.export_fast_bsk(), ref.bsk2)
+    eng.close()
+
+
+@pytest.mark.parametrize("P,dbits", [(8, 3), (11, 4)])
+def test_sign_toy_fast_gadget_vs_oracle(need_gpu, oracle_lib, P, dbits):
+    """Per-round gadgets on the GPU: the leading sign_precise_rounds bootstraps
+    on the main key, the rest on the fast one, every value exact, and the sign
+    ciphertexts' phases track the oracle's two-key restatement."""
+    from fheicp.params import sign_plan, sign_rounds
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=dbits, **TOY_FAST)
+    d, j = sign_plan(prm)
+    assert 0 < j < len(sign_rounds(P, d))
+    eng = Engine(prm, 0)
+    eng.keygen(4321)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 4321)
+    v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
+    sign = eng.sign(eng.encrypt(v, seed=61))
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    h = 2 ** (P - 1)
+    sel = np.array([0, 1, h - 1, h, h + 1, 2 * h - 1])
+    s_ref = ref.sign_extract(ref.encrypt_ints(v[sel], seed=61, id0=0))
+    assert np.array_equal(ref.decrypt_bits(s_ref), (v[sel] < 0).astype(np.int64))
+    dph = signed(u64(eng.phase(sign[sel].contiguous())) - ref.phase(s_ref))
+    assert np.abs(dph).max() < 2 ** 56
+    # imported keys: the fast key is re-encrypted with fresh randomness, the
+    # signs are unchanged
+    eng2 = Engine(prm, 0)
+    eng2.import_keys(eng.export_keys())
+    assert not np.array_equal(eng2.export_fast_bsk(), eng.export_fast_bsk())
+    sign2 = eng2.sign(eng2.encrypt(v, seed=62))
+    assert np.array_equal(eng2.decrypt_bits(sign2).cpu().numpy(), (v < 0).astype(np.int64))
+    eng2.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("P,dbits,fast", [(16, 0, True), (16, 3, True), (19, 0, True), (19, 0, False),
+                                          (21, 0, True), (21, 0, False)])
+def test_sign_real_params(need_gpu, P, dbits, fast):
     """Real parameters at the C2/C4 (P=16: 4-bit digits, and 3-bit forced)
-    and C3 (P=21: 3-bit) widths, boundaries included."""
-    eng = Engine(replace(params_for_bits(P), sign_digit_bits=dbits), 0)
+    and C3 (P=21: 3-bit) widths, with (fast) and without the per-round fast
+    gadget, boundaries included."""
+    eng = Engine(replace(params_for_bits(P, fast=fast), sign_digit_bits=dbits), 0)
     eng.keygen(900 + P)
     rng = np.random.default_rng(P)
     h = 2 ** (P - 1)

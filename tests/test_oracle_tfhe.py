@@ -160,3 +160,28 @@ def test_pbs_lut_staircase(toy_ref):
     out = toy_ref.pbs_lut(sm, 0, 1 << 50, 2)
     err = toy_ref.phase(out).view(np.int64) - (D.astype(np.int64) << 50)
     assert np.abs(err).max() < 2 ** 45
+
+
+TOY_FAST = {"pbs_base_log": 12, "pbs_level": 3, "pbs_fast_base_log": 8, "pbs_fast_level": 2}
+
+
+@pytest.mark.parametrize("P,d", [(5, 4), (8, 3), (11, 4)])
+def test_sign_extract_fast_gadget_values(oracle_lib, P, d):
+    """Per-round gadgets: a toy set whose fast gadget (8, 2) is too coarse for
+    the leading rounds, so sign_plan splits the rounds between the two keys
+    (j main rounds, the rest on bsk2); every P-bit value (P <= 8; boundaries
+    and a sample above) keeps its sign."""
+    from dataclasses import replace
+    from fheicp.params import TOY, sign_plan, sign_rounds
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=d, **TOY_FAST)
+    dd, j = sign_plan(prm)
+    assert dd == d and (j < len(sign_rounds(P, d)) or P == 5)
+    r = oracle_lib.RefTFHE(prm.as_dict(), 4321)
+    assert r.bsk2 is not None and oracle_lib.sign_precise_rounds(prm.as_dict()) == j
+    h = 2 ** (P - 1)
+    v = np.arange(-h, h, dtype=np.int64)
+    if P > 8:
+        v = np.concatenate([[-h, -h + 1, -2, -1, 0, 1, h - 2, h - 1],
+                            np.random.default_rng(P).integers(-h, h, 120)]).astype(np.int64)
+    sign = r.sign_extract(r.encrypt_ints(v, seed=200 + P))
+    assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))

@@ -8,7 +8,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from fheicp.params import PBS_GADGETS, TOY, params_for_bits, noise_report, sign_digit_bits, sign_pbs_count
+from fheicp.params import (PBS_GADGETS, TOY, params_for_bits, noise_report, sign_digit_bits, sign_pbs_count,
+                           sign_plan, sign_precise_rounds, sign_rounds)
 from fheicp.search import sharded_topk
 
 
@@ -29,9 +30,10 @@ def test_gadget_table_has_margin(pmax, beta, lvl):
 
 def _param_sets():
     for P in range(2, 28):
-        p = params_for_bits(P)
-        for d in (0, 3, 4):
-            yield p.with_msg_bits(P).__class__(**{**p.as_dict(), "sign_digit_bits": d})
+        for fast in (True, False):
+            p = params_for_bits(P, fast=fast)
+            for d in (0, 3, 4):
+                yield p.with_msg_bits(P).__class__(**{**p.as_dict(), "sign_digit_bits": d})
     for P in range(2, 17):
         yield TOY.with_msg_bits(P)
 
@@ -46,10 +48,33 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
         cp = _lib.params_struct(d)
         assert sign_digit_bits(p) == oracle_lib.sign_digit_bits(d) == L.fhe_sign_digit_bits(cp), d
         assert sign_pbs_count(p) == oracle_lib.sign_pbs_count(d) == L.fhe_sign_pbs_count(cp), d
+        assert sign_precise_rounds(p) == oracle_lib.sign_precise_rounds(d) == L.fhe_sign_precise_rounds(cp), d
     # the headline width: 4-bit digits at P = 16, 3-bit where 4 misses the bar
     assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 3, 3, 3]
     assert sign_pbs_count(16) == 7
     assert noise_report(params_for_bits(16))["digit_bits"] == 4
+
+
+def test_fast_gadget_plan():
+    """Per-round gadgets: P > 17 gets the (15, 2) gadget for
+    the sign rounds whose noise is barely amplified; only the leading rounds,
+    whose output is shifted up the most, stay on the precise gadget, and every
+    round keeps 9.2 sigma."""
+    from fheicp.params import _plan_worst
+    for P in range(4, 18):
+        assert params_for_bits(P).pbs_fast_level == 0
+    want = {18: (4, 1), 19: (4, 1), 20: (4, 2), 21: (3, 3), 22: (4, 3), 23: (3, 4), 24: (4, 4), 25: (3, 5),
+            26: (3, 6), 27: (3, 7)}
+    for P, dj in want.items():
+        p = params_for_bits(P)
+        assert (p.pbs_fast_base_log, p.pbs_fast_level) == (15, 2)
+        assert sign_plan(p) == dj, P
+        d, j = dj
+        assert _plan_worst(p, d, j) >= 9.2
+        assert j == 0 or _plan_worst(p, d, j - 1) < 9.2
+        assert len(sign_rounds(P, d)) == sign_pbs_count(p)
+    # without the fast gadget: all rounds on the one gadget, as before
+    assert sign_plan(params_for_bits(19, fast=False)) == (4, 9)
 
 
 def test_sign_digit_bits_validation():
