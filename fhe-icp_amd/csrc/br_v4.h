@@ -323,13 +323,19 @@ struct Acc<true> {
   using T = uint32_t;
   static __device__ __forceinline__ T from64(u64 x) { return (T)((x + (1ull << 31)) >> 32); }
   static __device__ __forceinline__ u64 to64(T x) { return (u64)x << 32; }
-  // round(z / 2^32) mod 2^32 via a magic number: z/2^32 + 1.5*2^55 has an
-  // ulp of 8, so its low mantissa word is round(z / 2^35) mod 2^32 for
-  // |z| < 2^86 (the product sums here stay below 2^85). The 3 dropped bits
-  // add noise far below sigma_pbs.
+  // round(z / 2^32) mod 2^32, exact for any z: f = fract(z / 2^64) is exact
+  // (a power-of-two scale, then dropping the integer part), and f * 2^32 +
+  // 1.5 * 2^52 has an ulp of 1, so its low mantissa word is round(f * 2^32).
+  // (Rounding at 2^35 instead, one fma, was measured to double the
+  // bootstrap noise: the output rounding is key-weighted like the gadget's.)
   static __device__ __forceinline__ T from_f64(double z) {
-    const double t = __fma_rn(z, 1.0 / 4294967296.0, 54043195528445952.0);
-    return (T)(uint32_t)__builtin_bit_cast(uint64_t, t) << 3;
+#ifdef FHEICP_A32_ROUND35  // A/B build only (tools/build_variant.sh)
+    const double t35 = __fma_rn(z, 1.0 / 4294967296.0, 54043195528445952.0);
+    return (T)(uint32_t)__builtin_bit_cast(uint64_t, t35) << 3;
+#endif
+    const double f = __builtin_amdgcn_fract(z * (1.0 / 18446744073709551616.0));
+    const double t = __fma_rn(f, 4294967296.0, 6755399441055744.0);
+    return (T)(uint32_t)__builtin_bit_cast(uint64_t, t);
   }
 };
 template <>

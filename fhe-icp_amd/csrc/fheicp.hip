@@ -47,9 +47,10 @@ struct fhe_ctx {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool prof = false;
-  ProfAcc prof_br, prof_ks;
+  ProfAcc prof_br, prof_br_fast, prof_ks;  // blind rotation on the main / fast gadget
   int v4_g = 4;        // v4 ciphertexts per workgroup (FHEICP_V4_G = 1, 2 or 4)
   int v4_fl = 0;       // v4 per-ciphertext LDS hand-offs instead of s_barrier (FHEICP_V4_FL=1)
+  int v4_a64 = 0;      // v4: 64-bit accumulators even where 32 bits suffice (FHEICP_V4_A64=1, A/B)
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2, 3
   int v4_dbg = 0;      // timing experiments only (FHEICP_V4_DBG), wrong results
   // i8-MFMA key switch: key byte planes and a digit/body workspace
@@ -233,6 +234,7 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
     ctx->v4_g = (g == 1 || g == 2 || g == 4) ? g : 4;
   }
   if (const char* e = getenv("FHEICP_V4_FL")) ctx->v4_fl = atoi(e) != 0;
+  if (const char* e = getenv("FHEICP_V4_A64")) ctx->v4_a64 = atoi(e) != 0;
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
   if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
@@ -307,6 +309,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     hipFree(ctx->bsk2); hipFree(ctx->bsk2_fft);
     hipFree(ctx->ksk8); hipFree(ctx->ks_ws); hipFree(ctx->tw4);
     free_ev(ctx->prof_br);
+    free_ev(ctx->prof_br_fast);
     free_ev(ctx->prof_ks);
   }
   delete ctx;
@@ -669,7 +672,8 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   const c64* bsk_fft = fast ? ctx->bsk2_fft : ctx->bsk_fft;
   const int var = variant_for(ctx, p);
   hipEvent_t e1;
-  prof_begin(ctx, ctx->prof_br, st, &e1);
+  ProfAcc& prof = fast ? ctx->prof_br_fast : ctx->prof_br;
+  prof_begin(ctx, prof, st, &e1);
   const dim3 g((unsigned)count), b(64);
 #define BR(LOGM, K)                                                                                           \
   hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
@@ -713,7 +717,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       default: BR4D(63); break;
     }
   } else if (p.N == 1024 && p.k == 2 && var == 4) {
-    const bool a32 = p.pbs_level * p.pbs_base_log <= 31;
+    const bool a32 = p.pbs_level * p.pbs_base_log <= 31 && !ctx->v4_a64;
     switch (p.pbs_level) {
       case 1: if (a32) BR4(1, true); else BR4(1, false); break;
       case 2: if (a32) BR4(2, true); else BR4(2, false); break;
@@ -735,7 +739,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
 #undef BR4G
 #undef BR4F
 #undef BRV
-  prof_end(ctx, ctx->prof_br, st, e1, count);
+  prof_end(ctx, prof, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -1083,23 +1087,30 @@ int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t
   int rc = need_device(ctx);
   if (rc) return rc;
   if (!kernel) return fail(ctx, FHE_E_ARG, "null kernel name");
-  ProfAcc* a = nullptr;
-  if (!strcmp(kernel, "blind_rotate")) a = &ctx->prof_br;
-  else if (!strcmp(kernel, "keyswitch")) a = &ctx->prof_ks;
+  std::vector<ProfAcc*> acc;
+  if (!strcmp(kernel, "blind_rotate")) acc = {&ctx->prof_br, &ctx->prof_br_fast};
+  else if (!strcmp(kernel, "blind_rotate_main")) acc = {&ctx->prof_br};
+  else if (!strcmp(kernel, "blind_rotate_fast")) acc = {&ctx->prof_br_fast};
+  else if (!strcmp(kernel, "keyswitch")) acc = {&ctx->prof_ks};
   else return fail(ctx, FHE_E_ARG, "unknown kernel name");
   double ms = 0;
-  for (auto& e : a->ev) {
-    HIPCHK(ctx, hipEventSynchronize(e.second));
-    float x = 0;
-    HIPCHK(ctx, hipEventElapsedTime(&x, e.first, e.second));
-    ms += x;
+  int64_t nl = 0, it = 0;
+  for (ProfAcc* a : acc) {
+    for (auto& e : a->ev) {
+      HIPCHK(ctx, hipEventSynchronize(e.second));
+      float x = 0;
+      HIPCHK(ctx, hipEventElapsedTime(&x, e.first, e.second));
+      ms += x;
+    }
+    nl += a->launches;
+    it += a->items;
+    free_ev(*a);
+    a->launches = 0;
+    a->items = 0;
   }
   if (total_ms) *total_ms = ms;
-  if (launches) *launches = a->launches;
-  if (items) *items = a->items;
-  free_ev(*a);
-  a->launches = 0;
-  a->items = 0;
+  if (launches) *launches = nl;
+  if (items) *items = it;
   return FHE_OK;
 }
 

@@ -316,7 +316,11 @@ template <int L, bool A32>
 __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int beta, int (&d)[L]) {
   const int prec = L * beta;
   if constexpr (A32) {
-    uint32_t r = ((x >> (31 - prec)) + 1) >> 1;
+    // x is a whole number of 2^32 units: ties (x at exactly half a step) are
+    // frequent, so round them to even, or the rounding error has a mean that
+    // the key-weighted sum would turn into a phase bias
+    const int sh = 32 - prec;
+    uint32_t r = (x + ((1u << (sh - 1)) - 1u) + ((x >> sh) & 1u)) >> sh;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       const int di = __builtin_amdgcn_sbfe((int)r, i * beta, beta);

@@ -54,7 +54,13 @@ class SchemeParams:
 # (sign_digit_bits) are used where they too keep 9.2 sigma.
 PBS_GADGETS = ((17, 15, 2), (21, 12, 3), (23, 10, 4), (25, 8, 5), (26, 7, 6), (27, 6, 7))
 SIGMA_BAR = 9.2
-FAST_GADGET = (15, 2)
+# candidate fast gadgets for the low-amplification sign rounds, and the
+# blind-rotation time per bootstrap by level relative to L = 2, measured on
+# MI355X at 1024 ciphertexts (v4 kernels for L <= 3; L = 1 and 2 on 32-bit
+# accumulators, L = 3 on 64-bit; tools/ab_gadgets.sh): 7.8 / 12.0 / 21 ms.
+# L >= 4 (v2 kernel) is extrapolated; only the ranking matters.
+FAST_GADGETS = ((15, 2), (23, 1))
+BR_COST = {1: 0.65, 2: 1.0, 3: 1.8, 4: 2.6, 5: 3.2, 6: 3.8, 7: 4.4, 8: 5.0}
 
 
 def sign_rounds(P: int, d: int):
@@ -141,18 +147,33 @@ def sign_pbs_count(p) -> int:
     return 2 * (m // d) + (2 if r >= 3 else r) + 1
 
 
+def plan_cost(p: SchemeParams) -> float:
+    """Relative time of one sign extraction: its bootstraps weighted by
+    BR_COST of the gadget each runs on (sign_plan)."""
+    P = p.msg_bits
+    if P < 4:
+        return P * BR_COST[p.pbs_level]
+    d, j = sign_plan(p)
+    R = len(sign_rounds(P, d))
+    return j * BR_COST[p.pbs_level] + (R - j) * BR_COST[p.pbs_fast_level or p.pbs_level]
+
+
 def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
-    """The gadget of PBS_GADGETS for width P; with fast, P > 17 also gets the
-    (15, 2) gadget for the sign rounds that do not need the precise one, if
-    the plan puts at least one round on it."""
+    """The gadget of PBS_GADGETS for width P; with fast, also the candidate
+    of FAST_GADGETS (other than the main gadget) whose sign plan is cheapest
+    by BR_COST, if it beats the single-gadget plan."""
     for pmax, beta, lvl in PBS_GADGETS:
         if P <= pmax:
             p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
-            if fast and (beta, lvl) != FAST_GADGET:
-                q = replace(p, pbs_fast_base_log=FAST_GADGET[0], pbs_fast_level=FAST_GADGET[1])
-                d, j = sign_plan(q)
-                if j < len(sign_rounds(P, d)):
-                    p = q
+            if fast and P >= 4:
+                best = plan_cost(p)
+                for fb, fl in FAST_GADGETS:
+                    if (fb, fl) == (beta, lvl):
+                        continue
+                    q = replace(p, pbs_fast_base_log=fb, pbs_fast_level=fl)
+                    c = plan_cost(q)
+                    if c < best - 1e-9:
+                        p, best = q, c
             return p
     raise ValueError(f"accumulator width P={P} exceeds the supported 27 bits")
 

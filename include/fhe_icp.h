@@ -237,7 +237,9 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
  * When enabled, every blind-rotation (external-product) and key-switch
  * launch is bracketed by hipEvents on its own stream. fhe_profile_read
  * synchronises and returns total milliseconds, launch count and ciphertexts
- * processed for kernel "blind_rotate" or "keyswitch", then resets them. */
+ * processed for kernel "blind_rotate" (both gadgets), "blind_rotate_main",
+ * "blind_rotate_fast" (fhe_params.pbs_fast_*) or "keyswitch", then resets
+ * what it read. */
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
 /* Development aid: 4 x 16 s_memtime phase stamps of one wave of the v4 blind

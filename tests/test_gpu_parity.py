@@ -215,11 +215,12 @@ def test_sign_toy_all_values_vs_oracle(need_gpu, oracle_lib, P, dbits):
 TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_level=2)
 
 
-@pytest.mark.parametrize("P", [8, 19])
+@pytest.mark.parametrize("P", [8, 16, 19])
 def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P):
     """Both bootstrapping keys of a two-gadget parameter set (toy (12,3)+(8,2);
-    real P=19: (12,3)+(15,2)) are bit-exact against the oracle's keygen."""
-    prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 17 else params_for_bits(P)
+    real P=16: (15,2)+(23,1); P=19: (12,3)+(15,2)) are bit-exact against the
+    oracle's keygen."""
+    prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 12 else params_for_bits(P)
     assert prm.pbs_fast_level
     eng = Engine(prm, 0)
     eng.keygen(4321)

@@ -56,25 +56,27 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
 
 
 def test_fast_gadget_plan():
-    """Per-round gadgets: P > 17 gets the (15, 2) gadget for
-    the sign rounds whose noise is barely amplified; only the leading rounds,
-    whose output is shifted up the most, stay on the precise gadget, and every
-    round keeps 9.2 sigma."""
-    from fheicp.params import _plan_worst
-    for P in range(4, 18):
-        assert params_for_bits(P).pbs_fast_level == 0
-    want = {18: (4, 1), 19: (4, 1), 20: (4, 2), 21: (3, 3), 22: (4, 3), 23: (3, 4), 24: (4, 4), 25: (3, 5),
-            26: (3, 6), 27: (3, 7)}
-    for P, dj in want.items():
+    """Per-round gadgets: params_for_bits adds the cheapest
+    fast gadget (by BR_COST) for the sign rounds whose noise is barely
+    amplified; only the leading rounds, whose output is shifted up the most,
+    stay on the precise gadget, and every round keeps 9.2 sigma."""
+    from fheicp.params import _plan_worst, plan_cost
+    want = {4: ((23, 1), 4, 0), 9: ((23, 1), 4, 0), 12: ((23, 1), 4, 1), 16: ((23, 1), 4, 3),
+            17: ((23, 1), 3, 5), 18: ((15, 2), 4, 1), 19: ((15, 2), 4, 1), 20: ((15, 2), 4, 2),
+            21: ((15, 2), 3, 3), 22: ((15, 2), 4, 3), 23: ((15, 2), 3, 4), 24: ((15, 2), 4, 4),
+            25: ((15, 2), 3, 5), 26: ((15, 2), 3, 6), 27: ((15, 2), 3, 7)}
+    for P, (fg, d, j) in want.items():
         p = params_for_bits(P)
-        assert (p.pbs_fast_base_log, p.pbs_fast_level) == (15, 2)
-        assert sign_plan(p) == dj, P
-        d, j = dj
+        assert (p.pbs_fast_base_log, p.pbs_fast_level) == fg, P
+        assert sign_plan(p) == (d, j), P
         assert _plan_worst(p, d, j) >= 9.2
         assert j == 0 or _plan_worst(p, d, j - 1) < 9.2
         assert len(sign_rounds(P, d)) == sign_pbs_count(p)
-    # without the fast gadget: all rounds on the one gadget, as before
+        assert plan_cost(p) < plan_cost(params_for_bits(P, fast=False))
+    # the headline width keeps its 4-bit digits and the single-gadget worst round
+    assert sign_plan(params_for_bits(16)) == (4, 3)
     assert sign_plan(params_for_bits(19, fast=False)) == (4, 9)
+    assert params_for_bits(3).pbs_fast_level == 0
 
 
 def test_sign_digit_bits_validation():

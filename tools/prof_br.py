@@ -20,16 +20,26 @@ ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--P", type=int, default=16)
 ap.add_argument("--variants", default="4,2")
 ap.add_argument("--dbg", default="", help="comma list of FHEICP_V4_DBG values to time (v4 only; wrong results)")
+ap.add_argument("--gadget", default="", help="base_log,level to override the bootstrap gadget")
+ap.add_argument("--lib", default="", help="load this libfheicp build instead (tools/build_variant.sh)")
 ap.add_argument("--stamps", action="store_true", help="print v4 phase timestamps (FHEICP_V4_DBG=128)")
 a = ap.parse_args()
 import os
+if a.lib:
+    from fheicp import _lib
+    _lib.LIB_PATH = Path(a.lib).resolve()
 runs = [(v, "0") for v in a.variants.split(",")] + [("4", d) for d in a.dbg.split(",") if d]
 if a.stamps:
     runs.append(("4", "128"))
 for var, dbg in runs:
     os.environ["FHEICP_BR_VARIANT"] = var
     os.environ["FHEICP_V4_DBG"] = dbg
-    eng = Engine(params_for_bits(a.P), 0)
+    prm = params_for_bits(a.P, fast=False)
+    if a.gadget:
+        from dataclasses import replace
+        gb, gl = (int(x) for x in a.gadget.split(","))
+        prm = replace(prm, pbs_base_log=gb, pbs_level=gl)
+    eng = Engine(prm, 0)
     eng.keygen(7)
     v = np.random.default_rng(1).integers(-(2 ** (a.P - 1)), 2 ** (a.P - 1), a.B)
     ct = eng.encrypt(v, seed=3)
@@ -38,6 +48,15 @@ for var, dbg in runs:
         sm = eng.keyswitch(ct, a.P - 1 - i, 1 << 62)
         out = eng.pbs(sm, 1 << 62)
     torch.cuda.synchronize()
+    # output noise of the last bootstrap: phase - nearest of +-2^62
+    ph = eng.phase(out).cpu().numpy().view(np.uint64)
+    err = (ph - np.uint64(1 << 62)).view(np.int64).astype(np.float64)
+    err2 = (ph + np.uint64(1 << 62)).view(np.int64).astype(np.float64)
+    e = np.where(np.abs(err) < np.abs(err2), err, err2)
+    from fheicp.params import _variances
+    print(f"gadget=({prm.pbs_base_log},{prm.pbs_level}) output noise log2 std {np.log2(e.std() / 2.0 ** 64):.2f} "
+          f"(model {0.5 * np.log2(_variances(prm)[0]):.2f}) "
+          f"(max |e| 2^{np.log2(np.abs(e).max() / 2.0 ** 64):.2f} of the torus)")
     br = eng.profile_read("blind_rotate")
     ks = eng.profile_read("keyswitch")
     if dbg == "128":
@@ -68,6 +87,6 @@ for var, dbg in runs:
         late = int((start > 0.1 * end.max()).sum())
         print(f"  workgroups starting after 10% of the span: {late}; distinct (se, sh, cu): "
               f"{len(set(zip(se.tolist(), sh.tolist(), cu.tolist())))}")
-    print(f"variant={var} dbg={dbg} B={a.B} blind_rotate {br['total_ms'] / br['launches']:.3f} ms/launch "
+    print(f"variant={var} dbg={dbg} G={os.environ.get('FHEICP_V4_G', '4')} A64={os.environ.get('FHEICP_V4_A64', '0')} B={a.B} blind_rotate {br['total_ms'] / br['launches']:.3f} ms/launch "
           f"({a.B * br['launches'] / br['total_ms'] * 1e3:.0f} PBS/s), keyswitch {ks['total_ms'] / ks['launches']:.3f} ms/launch")
     eng.close()

@@ -9,6 +9,7 @@ Usage: traffic.py <fetch_counters.csv> <write_counters.csv> [out.json]
 """
 import csv
 import json
+import os
 import sys
 
 
@@ -32,6 +33,8 @@ def main():
         "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
         "recipe": "(2*FETCH_SIZE + WRITE_SIZE) * 1024, separate --pmc passes (gfx950 FETCH_SIZE half-count)",
     }
+    # what was measured (gadget, kernel build), from $TRAFFIC_META (JSON)
+    out.update(json.loads(os.environ.get("TRAFFIC_META", "{}")))
     s = json.dumps(out, indent=2)
     print(s)
     if len(sys.argv) > 3:
