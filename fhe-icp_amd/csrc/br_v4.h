@@ -140,7 +140,10 @@ __device__ __forceinline__ void ct_wait(const uint32_t* f, uint32_t target) {
 // ---- register-level pieces ---------------------------------------------
 constexpr double RH = 0.70710678118654752440;  // sqrt(2)/2
 
-// constant DFT-8 network, DIF (natural -> bit-reversed within the pass)
+// constant DFT-8 network, DIF (natural -> bit-reversed within the pass).
+// The w8 and w8^3 twiddles of elements 5 and 7 are (1 -+ i) * RH: the
+// (1 -+ i) part is two adds, and the RH factor is carried through the bit-1
+// butterfly (which mixes only 5 and 7) into the bit-0 butterflies as FMAs.
 __device__ __forceinline__ void dft8(c64 (&v)[S]) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {  // slot bit 2; twiddles 1, w8, i, w8^3
@@ -148,9 +151,9 @@ __device__ __forceinline__ void dft8(c64 (&v)[S]) {
     v[u] = cadd(X, Y);
     const c64 D = csub(X, Y);
     if (u == 0) v[4] = D;
-    if (u == 1) v[5] = {(D.x - D.y) * RH, (D.x + D.y) * RH};
+    if (u == 1) v[5] = {D.x - D.y, D.x + D.y};        // / RH
     if (u == 2) v[6] = {-D.y, D.x};
-    if (u == 3) v[7] = {-(D.x + D.y) * RH, (D.x - D.y) * RH};
+    if (u == 3) v[7] = {-(D.x + D.y), D.x - D.y};     // / RH
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {  // slot bit 1; twiddles 1, i
@@ -163,11 +166,17 @@ __device__ __forceinline__ void dft8(c64 (&v)[S]) {
 #pragma unroll
   for (int u = 0; u < S; u += 2) {  // slot bit 0
     const c64 X = v[u], Y = v[u + 1];
-    v[u] = cadd(X, Y);
-    v[u + 1] = csub(X, Y);
+    if (u >= 4) {  // v[5], v[7] still lack their RH factor
+      v[u] = {__fma_rn(Y.x, RH, X.x), __fma_rn(Y.y, RH, X.y)};
+      v[u + 1] = {__fma_rn(Y.x, -RH, X.x), __fma_rn(Y.y, -RH, X.y)};
+    } else {
+      v[u] = cadd(X, Y);
+      v[u + 1] = csub(X, Y);
+    }
   }
 }
-// its exact inverse up to a factor 8 (DIT, conjugate constants)
+// its exact inverse up to a factor 8 (DIT, conjugate constants); the RH of
+// the exp(-i pi/4) and exp(-3 i pi/4) twiddles goes into the last butterflies
 __device__ __forceinline__ void idft8(c64 (&v)[S]) {
 #pragma unroll
   for (int u = 0; u < S; u += 2) {
@@ -186,12 +195,16 @@ __device__ __forceinline__ void idft8(c64 (&v)[S]) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const c64 X = v[u], Y0 = v[u + 4];
-    c64 Y = Y0;
-    if (u == 1) Y = {(Y0.x + Y0.y) * RH, (Y0.y - Y0.x) * RH};    // * exp(-i pi/4)
-    if (u == 2) Y = {Y0.y, -Y0.x};                               // * -i
-    if (u == 3) Y = {(Y0.y - Y0.x) * RH, -(Y0.x + Y0.y) * RH};   // * exp(-3 i pi/4)
-    v[u] = cadd(X, Y);
-    v[u + 4] = csub(X, Y);
+    if (u == 1 || u == 3) {
+      // u = 1: * exp(-i pi/4) = RH (1 - i); u = 3: * exp(-3 i pi/4) = RH (-1 - i)
+      const c64 Y = (u == 1) ? c64{Y0.x + Y0.y, Y0.y - Y0.x} : c64{Y0.y - Y0.x, -(Y0.x + Y0.y)};
+      v[u] = {__fma_rn(Y.x, RH, X.x), __fma_rn(Y.y, RH, X.y)};
+      v[u + 4] = {__fma_rn(Y.x, -RH, X.x), __fma_rn(Y.y, -RH, X.y)};
+    } else {
+      const c64 Y = (u == 2) ? c64{Y0.y, -Y0.x} : Y0;  // * -i
+      v[u] = cadd(X, Y);
+      v[u + 4] = csub(X, Y);
+    }
   }
 }
 
@@ -323,17 +336,18 @@ struct Acc<true> {
   using T = uint32_t;
   static __device__ __forceinline__ T from64(u64 x) { return (T)((x + (1ull << 31)) >> 32); }
   static __device__ __forceinline__ u64 to64(T x) { return (u64)x << 32; }
-  // round(z / 2^32) mod 2^32, exact for any z: f = fract(z / 2^64) is exact
-  // (a power-of-two scale, then dropping the integer part), and f * 2^32 +
-  // 1.5 * 2^52 has an ulp of 1, so its low mantissa word is round(f * 2^32).
+  // round(z / 2^32) mod 2^32, exact for any z, from t = z / 2^64 (the
+  // FFT-domain BSK carries the 2^-64, k_bsk_to_fft_v4): f = fract(t) is
+  // exact, and f * 2^32 + 1.5 * 2^52 has an ulp of 1, so its low mantissa
+  // word is round(f * 2^32).
   // (Rounding at 2^35 instead, one fma, was measured to double the
   // bootstrap noise: the output rounding is key-weighted like the gadget's.)
   static __device__ __forceinline__ T from_f64(double z) {
 #ifdef FHEICP_A32_ROUND35  // A/B build only (tools/build_variant.sh)
-    const double t35 = __fma_rn(z, 1.0 / 4294967296.0, 54043195528445952.0);
+    const double t35 = __fma_rn(z, 4294967296.0, 54043195528445952.0);
     return (T)(uint32_t)__builtin_bit_cast(uint64_t, t35) << 3;
 #endif
-    const double f = __builtin_amdgcn_fract(z * (1.0 / 18446744073709551616.0));
+    const double f = __builtin_amdgcn_fract(z);
     const double t = __fma_rn(f, 4294967296.0, 6755399441055744.0);
     return (T)(uint32_t)__builtin_bit_cast(uint64_t, t);
   }

@@ -340,6 +340,10 @@ static int need_keys(fhe_ctx* ctx) {
 
 // blind-rotation kernel for a gadget: the requested variant (4 unless
 // FHEICP_BR_VARIANT), falling back to v2 where v4 does not apply
+// the v4 kernel keeps 32-bit accumulators for this gadget
+static bool v4_a32(const fhe_ctx* ctx, const fhe_params& q) {
+  return q.pbs_level * q.pbs_base_log <= 31 && !ctx->v4_a64;
+}
 static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
   if (ctx->br_variant == 4 &&
       !(q.k == 2 && q.n <= v4::NMAX && q.pbs_level <= 3 && (q.pbs_level == 1 || q.pbs_base_log <= 16)))
@@ -378,7 +382,7 @@ static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* b
     case 1024:
       if (variant_for(ctx, p) == 4)
         hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, bsk, npoly, ctx->tw4,
-                           bsk_fft);
+                           bsk_fft, (v4_a32(ctx, p) ? 1.0 / 18446744073709551616.0 : 1.0) / (double)(p.N / 2));
       else if (variant_for(ctx, p) == 3)
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
       else
@@ -704,7 +708,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
     else BR4G(2, true, D, 4);                        \
   } while (0)
   if (p.N == 1024 && p.k == 2 && var == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
-      p.pbs_level * p.pbs_base_log <= 31) {
+      v4_a32(ctx, p)) {
     switch (ctx->v4_dbg) {
       case 1: BR4D(1); break;
       case 2: BR4D(2); break;
@@ -717,7 +721,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       default: BR4D(63); break;
     }
   } else if (p.N == 1024 && p.k == 2 && var == 4) {
-    const bool a32 = p.pbs_level * p.pbs_base_log <= 31 && !ctx->v4_a64;
+    const bool a32 = v4_a32(ctx, p);
     switch (p.pbs_level) {
       case 1: if (a32) BR4(1, true); else BR4(1, false); break;
       case 2: if (a32) BR4(2, true); else BR4(2, false); break;
