@@ -110,7 +110,7 @@ def br_flops_per_ct(p) -> float:
 
 def read_br(eng) -> dict:
     """Blind-rotation HIP-event totals per gadget (fhe_profile_read)."""
-    return {"main": eng.profile_read("blind_rotate_main"), "fast": eng.profile_read("blind_rotate_fast")}
+    return {g: eng.profile_read(f"blind_rotate_{g}") for g in ("main", "fast", "fast2")}
 
 
 def _br_kernel(q, br) -> dict:
@@ -134,12 +134,14 @@ def _br_kernel(q, br) -> dict:
 def roofline(p, brs) -> dict:
     """External-product (blind rotation) roofline of the dominant kernel, from
     the HIP events bracketing each launch on its stream (fhe_profile_read).
-    With a fast gadget the sign rounds run two kernels; the
-    one with the larger total time is reported, both are listed."""
+    With fast gadgets the sign rounds run two or three
+    kernels; the one with the larger total time is reported, all are listed."""
     from dataclasses import replace
     qs = {"main": p}
     if p.pbs_fast_level:
         qs["fast"] = replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level)
+    if p.pbs_fast2_level:
+        qs["fast2"] = replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level)
     ks = {g: _br_kernel(q, brs[g]) for g, q in qs.items() if brs[g]["launches"]}
     dom = max(ks, key=lambda g: ks[g]["total_ms"])
     k = ks[dom]

@@ -41,13 +41,15 @@ struct fhe_ctx {
   bool keys = false;
   u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
   c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr, *tw4 = nullptr;
-  u64* bsk2 = nullptr;      // fast-gadget bootstrapping key (p.pbs_fast_*), coefficient domain
-  c64* bsk2_fft = nullptr;  // ... and its FFT form
+  // bootstrapping keys of the fast gadgets (p.pbs_fast_*, p.pbs_fast2_*),
+  // coefficient domain and FFT form
+  u64* bskf[2] = {nullptr, nullptr};
+  c64* bskf_fft[2] = {nullptr, nullptr};
   // workspace
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool prof = false;
-  ProfAcc prof_br, prof_br_fast, prof_ks;  // blind rotation on the main / fast gadget
+  ProfAcc prof_br, prof_brf[2], prof_ks;  // blind rotation on the main / fast / fast2 gadget
   int v4_g = 4;        // v4 ciphertexts per workgroup (FHEICP_V4_G = 1, 2 or 4)
   int v4_fl = 0;       // v4 per-ciphertext LDS hand-offs instead of s_barrier (FHEICP_V4_FL=1)
   int v4_a64 = 0;      // v4: 64-bit accumulators even where 32 bits suffice (FHEICP_V4_A64=1, A/B)
@@ -105,6 +107,11 @@ static int validate(const fhe_params* p, std::string& why) {
       p->pbs_fast_base_log < 0 || p->pbs_fast_level * p->pbs_fast_base_log > 62) {
     why = "fast pbs decomposition out of range (0, 0 for none)"; return -1;
   }
+  if ((p->pbs_fast2_base_log == 0) != (p->pbs_fast2_level == 0) || p->pbs_fast2_level < 0 ||
+      p->pbs_fast2_level > 8 || p->pbs_fast2_base_log < 0 || p->pbs_fast2_level * p->pbs_fast2_base_log > 62 ||
+      (p->pbs_fast2_level && !p->pbs_fast_level)) {
+    why = "fast2 pbs decomposition out of range (0, 0 for none; needs a fast gadget)"; return -1;
+  }
   return 0;
 }
 
@@ -149,49 +156,62 @@ static int sign_rounds(int P, int d, int* shift, int* mlog) {
   add(0, -(d + 1));
   return R;
 }
-// worst margin (sigmas) over all rounds when rounds < j use the main gadget
-static double plan_worst(const fhe_params& p, int d, int j) {
+// worst margin (sigmas) over all rounds when rounds < j1 use the main gadget,
+// rounds < j2 the fast one and the rest the fast2 one
+static double plan_worst(const fhe_params& p, int d, int j1, int j2) {
   int sh[64], ml[64];
   const int R = sign_rounds(p.msg_bits, d, sh, ml);
-  const double vm = pbs_var(p, p.pbs_base_log, p.pbs_level), vf = pbs_var(p, p.pbs_fast_base_log, p.pbs_fast_level);
+  const double vm = pbs_var(p, p.pbs_base_log, p.pbs_level);
+  const double vf = p.pbs_fast_level ? pbs_var(p, p.pbs_fast_base_log, p.pbs_fast_level) : vm;
+  const double vf2 = p.pbs_fast2_level ? pbs_var(p, p.pbs_fast2_base_log, p.pbs_fast2_level) : vf;
   const double fixed = ks_var(p) + ms_var(p);
   double acc = 0, worst = 1e300;
   for (int r = 0; r < R; ++r) {
     worst = std::min(worst, std::ldexp(1.0, ml[r]) / std::sqrt(acc * std::ldexp(1.0, 2 * sh[r]) + fixed));
-    acc += r < j ? vm : vf;
+    acc += r < j1 ? vm : r < j2 ? vf : vf2;
   }
-  return worst;
+  // the last bootstrap's output is the sign ciphertext: decryptable at 1/4
+  const double vl = R - 1 < j1 ? vm : R - 1 < j2 ? vf : vf2;
+  return std::min(worst, 0.25 / std::sqrt(vl));
 }
-// (d, j): digit width and how many leading bootstraps need the main gadget.
-// Without a fast gadget: the single-gadget rule (d = 4 if its worst round
-// keeps 9.2 sigma, else 3), all rounds on the main gadget. With one: the
-// widest d (or the forced one) and the fewest main-gadget rounds for which
-// every round keeps 9.2 sigma.
-static void sign_plan(const fhe_params& p, int* d_out, int* j_out) {
+// (d, j1, j2): digit width; bootstraps < j1 run on the main gadget, < j2 on
+// the fast one, the rest on the fast2 one. Without a fast gadget: the
+// single-gadget rule (d = 4 if its worst round keeps 9.2 sigma, else 3), all
+// rounds on the main gadget. With fast gadgets: the widest d (or the forced
+// one), then the fewest main rounds j1 for which some j2 keeps every round at
+// 9.2 sigma, then the fewest fast rounds (j2 = R without a fast2 gadget).
+static void sign_plan(const fhe_params& p, int* d_out, int* j1_out, int* j2_out) {
   int sh[64], ml[64];
   const int P = p.msg_bits;
-  if (P < 4) { *d_out = 0; *j_out = P; return; }
+  if (P < 4) { *d_out = 0; *j1_out = *j2_out = P; return; }
   if (!p.pbs_fast_level) {
     int d = 3;
     if (p.sign_digit_bits) d = std::min(p.sign_digit_bits, P);
     else if (digit_margin_sigmas(p, std::min(4, P)) >= 9.2) d = std::min(4, P);
     *d_out = d;
-    *j_out = sign_rounds(P, d, sh, ml);
+    *j1_out = *j2_out = sign_rounds(P, d, sh, ml);
     return;
   }
   const int first = p.sign_digit_bits ? std::min(p.sign_digit_bits, P) : std::min(4, P);
   const int last = p.sign_digit_bits ? first : 3;
   for (int d = first; d >= last; --d) {
     const int R = sign_rounds(P, d, sh, ml);
-    for (int j = 0; j <= R; ++j)
-      if (plan_worst(p, d, j) >= 9.2) { *d_out = d; *j_out = j; return; }
+    for (int j1 = 0; j1 <= R; ++j1) {
+      if (plan_worst(p, d, j1, R) < 9.2) continue;  // fast rounds only help from here
+      int j2 = R;
+      if (p.pbs_fast2_level)
+        for (j2 = j1; j2 < R && plan_worst(p, d, j1, j2) < 9.2; ++j2) {
+        }
+      *d_out = d; *j1_out = j1; *j2_out = j2;
+      return;
+    }
   }
   *d_out = last;
-  *j_out = sign_rounds(P, last, sh, ml);
+  *j1_out = *j2_out = sign_rounds(P, last, sh, ml);
 }
 static int sign_digits(const fhe_params& p) {
-  int d, j;
-  sign_plan(p, &d, &j);
+  int d, j1, j2;
+  sign_plan(p, &d, &j1, &j2);
   return d;
 }
 
@@ -306,10 +326,11 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     hipSetDevice(ctx->device);
     hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk); hipFree(ctx->ksk_colsum);
     hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
-    hipFree(ctx->bsk2); hipFree(ctx->bsk2_fft);
+    for (int g = 0; g < 2; ++g) hipFree(ctx->bskf[g]), hipFree(ctx->bskf_fft[g]);
     hipFree(ctx->ksk8); hipFree(ctx->ks_ws); hipFree(ctx->tw4);
     free_ev(ctx->prof_br);
-    free_ev(ctx->prof_br_fast);
+    free_ev(ctx->prof_brf[0]);
+    free_ev(ctx->prof_brf[1]);
     free_ev(ctx->prof_ks);
   }
   delete ctx;
@@ -350,19 +371,35 @@ static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
     return 2;
   return ctx->br_variant;
 }
-// the parameters seen through the fast gadget (same keys, other decomposition)
-static fhe_params fast_params(const fhe_params& p) {
+// the parameters seen through fast gadget g (1: pbs_fast_*, 2: pbs_fast2_*;
+// same secret keys, other decomposition and bootstrapping key)
+static int fast_level(const fhe_params& p, int g) { return g == 1 ? p.pbs_fast_level : p.pbs_fast2_level; }
+static fhe_params fast_params(const fhe_params& p, int g) {
   fhe_params q = p;
-  q.pbs_base_log = p.pbs_fast_base_log;
-  q.pbs_level = p.pbs_fast_level;
+  q.pbs_base_log = g == 1 ? p.pbs_fast_base_log : p.pbs_fast2_base_log;
+  q.pbs_level = fast_level(p, g);
   return q;
+}
+// the fast gadgets' keys under the ChaCha20 streams 9/10 and 11/12
+static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
+  const fhe_params& p = ctx->p;
+  const size_t shm = 8 * (size_t)p.N + p.N;
+  for (int g = 1; g <= 2; ++g) {
+    if (!fast_level(p, g)) continue;
+    const fhe_params q = fast_params(p, g);
+    hipLaunchKernelGGL(k_keygen_bsk, dim3(q.n * (q.k + 1) * q.pbs_level), dim3(256), shm, st, K, q.N, q.k,
+                       q.pbs_level, q.pbs_base_log, q.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bskf[g - 1],
+                       (uint32_t)(g == 1 ? TAG_BSK2_MASK : TAG_BSK3_MASK),
+                       (uint32_t)(g == 1 ? TAG_BSK2_NOISE : TAG_BSK3_NOISE));
+  }
 }
 static int alloc_keys(fhe_ctx* ctx) {
   const fhe_params& p = ctx->p;
-  if (p.pbs_fast_level && !ctx->bsk2) {
-    const fhe_params q = fast_params(p);
-    HIPCHK(ctx, hipMalloc(&ctx->bsk2, 8 * fhe_bsk_words(&q)));
-    HIPCHK(ctx, hipMalloc(&ctx->bsk2_fft, sizeof(c64) * fhe_bsk_words(&q) / 2));
+  for (int g = 1; g <= 2; ++g) {
+    if (!fast_level(p, g) || ctx->bskf[g - 1]) continue;
+    const fhe_params q = fast_params(p, g);
+    HIPCHK(ctx, hipMalloc(&ctx->bskf[g - 1], 8 * fhe_bsk_words(&q)));
+    HIPCHK(ctx, hipMalloc(&ctx->bskf_fft[g - 1], sizeof(c64) * fhe_bsk_words(&q) / 2));
   }
   if (ctx->s_small) return FHE_OK;
   HIPCHK(ctx, hipMalloc(&ctx->s_small, 8 * (size_t)p.n));
@@ -403,7 +440,8 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
                        ctx->ksk8);
   }
   bsk_to_fft(ctx, p, ctx->bsk, ctx->bsk_fft, st);
-  if (p.pbs_fast_level) bsk_to_fft(ctx, fast_params(p), ctx->bsk2, ctx->bsk2_fft, st);
+  for (int g = 1; g <= 2; ++g)
+    if (fast_level(p, g)) bsk_to_fft(ctx, fast_params(p, g), ctx->bskf[g - 1], ctx->bskf_fft[g - 1], st);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -426,10 +464,7 @@ int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream) {
   hipLaunchKernelGGL(k_keygen_bsk, dim3(rows_bsk), dim3(256), shm, st, K, p.N, p.k, p.pbs_level, p.pbs_base_log,
                      p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk, (uint32_t)TAG_BSK_MASK,
                      (uint32_t)TAG_BSK_NOISE);
-  if (p.pbs_fast_level)
-    hipLaunchKernelGGL(k_keygen_bsk, dim3(p.n * (p.k + 1) * p.pbs_fast_level), dim3(256), shm, st, K, p.N, p.k,
-                       p.pbs_fast_level, p.pbs_fast_base_log, p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk2,
-                       (uint32_t)TAG_BSK2_MASK, (uint32_t)TAG_BSK2_NOISE);
+  keygen_fast_bsks(ctx, K, st);
   hipLaunchKernelGGL(k_keygen_ksk, dim3(big * p.ks_level), dim3(256), 0, st, K, p.n, p.ks_level, p.ks_base_log,
                      p.lwe_noise_bits, ctx->s_small, ctx->s_big, ctx->ksk);
   HIPCHK(ctx, hipGetLastError());
@@ -457,14 +492,15 @@ int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64
   return FHE_OK;
 }
 
-int fhe_export_fast_bsk(fhe_ctx* ctx, uint64_t* h_bsk2) {
+int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk) {
   int rc = need_keys(ctx);
   if (rc) return rc;
-  if (!ctx->p.pbs_fast_level) return fail(ctx, FHE_E_STATE, "no fast gadget in these parameters");
-  if (!h_bsk2) return fail(ctx, FHE_E_ARG, "null buffer");
-  const fhe_params q = fast_params(ctx->p);
+  if (which != 1 && which != 2) return fail(ctx, FHE_E_ARG, "which must be 1 (fast) or 2 (fast2)");
+  if (!fast_level(ctx->p, which)) return fail(ctx, FHE_E_STATE, "no such fast gadget in these parameters");
+  if (!h_bsk) return fail(ctx, FHE_E_ARG, "null buffer");
+  const fhe_params q = fast_params(ctx->p, which);
   HIPCHK(ctx, hipDeviceSynchronize());
-  HIPCHK(ctx, hipMemcpy(h_bsk2, ctx->bsk2, 8 * fhe_bsk_words(&q), hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemcpy(h_bsk, ctx->bskf[which - 1], 8 * fhe_bsk_words(&q), hipMemcpyDeviceToHost));
   return FHE_OK;
 }
 
@@ -481,15 +517,12 @@ int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s
   HIPCHK(ctx, hipMemcpy(ctx->bsk, h_bsk, 8 * fhe_bsk_words(&p), hipMemcpyHostToDevice));
   HIPCHK(ctx, hipMemcpy(ctx->ksk, h_ksk, 8 * fhe_ksk_words(&p), hipMemcpyHostToDevice));
   if (p.pbs_fast_level) {
-    // the fast-gadget key is not part of the exported set: re-encrypt it
-    // under the imported secrets with fresh randomness
+    // the fast gadgets' keys are not part of the exported set: re-encrypt
+    // them under the imported secrets with fresh randomness
     ChaKey K;
     std::random_device rd;
     for (int i = 0; i < 8; ++i) K.w[i] = rd();
-    const size_t shm = 8 * (size_t)p.N + p.N;
-    hipLaunchKernelGGL(k_keygen_bsk, dim3(p.n * (p.k + 1) * p.pbs_fast_level), dim3(256), shm, nullptr, K, p.N, p.k,
-                       p.pbs_fast_level, p.pbs_fast_base_log, p.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bsk2,
-                       (uint32_t)TAG_BSK2_MASK, (uint32_t)TAG_BSK2_NOISE);
+    keygen_fast_bsks(ctx, K, nullptr);
     HIPCHK(ctx, hipGetLastError());
   }
   rc = convert_bsk(ctx, nullptr);
@@ -668,15 +701,16 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   return FHE_OK;
 }
 
-// gad = 1: the fast gadget and its key (fhe_params.pbs_fast_*), else the main one
+// gad = 1 / 2: the fast / fast2 gadget and its key (fhe_params.pbs_fast*_*),
+// else the main one
 static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv tv, int mode, uint64_t* out,
                      uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, hipStream_t st, int gad = 0) {
-  const bool fast = gad && ctx->p.pbs_fast_level;
-  const fhe_params p = fast ? fast_params(ctx->p) : ctx->p;
-  const c64* bsk_fft = fast ? ctx->bsk2_fft : ctx->bsk_fft;
+  const bool fast = gad > 0 && fast_level(ctx->p, gad);
+  const fhe_params p = fast ? fast_params(ctx->p, gad) : ctx->p;
+  const c64* bsk_fft = fast ? ctx->bskf_fft[gad - 1] : ctx->bsk_fft;
   const int var = variant_for(ctx, p);
   hipEvent_t e1;
-  ProfAcc& prof = fast ? ctx->prof_br_fast : ctx->prof_br;
+  ProfAcc& prof = fast ? ctx->prof_brf[gad - 1] : ctx->prof_br;
   prof_begin(ctx, prof, st, &e1);
   const dim3 g((unsigned)count), b(64);
 #define BR(LOGM, K)                                                                                           \
@@ -827,9 +861,20 @@ int fhe_sign_pbs_count(const fhe_params* params) {
 int fhe_sign_precise_rounds(const fhe_params* params) {
   std::string why;
   if (validate(params, why)) return -1;
-  int d, j;
-  sign_plan(*params, &d, &j);
-  return j;
+  int d, j1, j2;
+  sign_plan(*params, &d, &j1, &j2);
+  return j1;
+}
+
+int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_rounds, int32_t* fast_end) {
+  std::string why;
+  if (validate(params, why)) return FHE_E_ARG;
+  int d, j1, j2;
+  sign_plan(*params, &d, &j1, &j2);
+  if (digit_bits) *digit_bits = d;
+  if (main_rounds) *main_rounds = j1;
+  if (fast_end) *fast_end = j2;
+  return FHE_OK;
 }
 
 static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
@@ -846,12 +891,13 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
     }
     return FHE_OK;
   }
-  int d, j;
-  sign_plan(p, &d, &j);
+  int d, j1, j2;
+  sign_plan(p, &d, &j1, &j2);
   const int m = P - d;
-  int round = 0;  // bootstraps issued so far; rounds >= j use the fast gadget (sign_plan)
+  int round = 0;  // bootstraps issued so far: [0, j1) main, [j1, j2) fast, then fast2 (sign_plan)
   auto br = [&](BrTv tv, int mode, uint64_t* sign) -> int {
-    const int gad = round++ >= j;
+    const int r = round++;
+    const int gad = r < j1 ? 0 : r < j2 ? 1 : 2;
     return launch_br(ctx, small, count, tv, mode, nullptr, d_ct_v, nullptr, sign, st, gad);
   };
   // one c-bit digit at bit b: the pair of rounds on v << (P-b-c) centred by 2^(63-c)
@@ -1092,9 +1138,10 @@ int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t
   if (rc) return rc;
   if (!kernel) return fail(ctx, FHE_E_ARG, "null kernel name");
   std::vector<ProfAcc*> acc;
-  if (!strcmp(kernel, "blind_rotate")) acc = {&ctx->prof_br, &ctx->prof_br_fast};
+  if (!strcmp(kernel, "blind_rotate")) acc = {&ctx->prof_br, &ctx->prof_brf[0], &ctx->prof_brf[1]};
   else if (!strcmp(kernel, "blind_rotate_main")) acc = {&ctx->prof_br};
-  else if (!strcmp(kernel, "blind_rotate_fast")) acc = {&ctx->prof_br_fast};
+  else if (!strcmp(kernel, "blind_rotate_fast")) acc = {&ctx->prof_brf[0]};
+  else if (!strcmp(kernel, "blind_rotate_fast2")) acc = {&ctx->prof_brf[1]};
   else if (!strcmp(kernel, "keyswitch")) acc = {&ctx->prof_ks};
   else return fail(ctx, FHE_E_ARG, "unknown kernel name");
   double ms = 0;

@@ -23,6 +23,8 @@ enum StreamTag : uint32_t {
   TAG_ENC_NOISE = 8,
   TAG_BSK2_MASK = 9,   // the fast-gadget bootstrapping key (fhe_params.pbs_fast_*)
   TAG_BSK2_NOISE = 10,
+  TAG_BSK3_MASK = 11,  // the fast2-gadget bootstrapping key (fhe_params.pbs_fast2_*)
+  TAG_BSK3_NOISE = 12,
 };
 
 struct ChaKey {

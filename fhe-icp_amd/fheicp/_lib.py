@@ -16,9 +16,10 @@ ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOM
 
 PARAM_FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
                 "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
-                "pbs_fast_base_log", "pbs_fast_level")
+                "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level")
 # fields a caller may leave out (0 = auto / none)
-OPTIONAL_FIELDS = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level")
+OPTIONAL_FIELDS = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log",
+                   "pbs_fast2_level")
 
 
 class FheParams(C.Structure):
@@ -46,7 +47,7 @@ SIGNATURES = [
     ("fhe_keygen_key", C.c_int, [_CTXP, C.POINTER(C.c_uint32), _vp]),
     ("fhe_export_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
     ("fhe_import_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
-    ("fhe_export_fast_bsk", C.c_int, [_CTXP, _vp]),
+    ("fhe_export_fast_bsk", C.c_int, [_CTXP, _i32, _vp]),
     ("fhe_encrypt_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _vp, _vp]),
     ("fhe_decrypt_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_decrypt_bits_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
@@ -59,6 +60,7 @@ SIGNATURES = [
     ("fhe_sign_digit_bits", C.c_int, [_P]),
     ("fhe_sign_pbs_count", C.c_int, [_P]),
     ("fhe_sign_precise_rounds", C.c_int, [_P]),
+    ("fhe_sign_plan", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     ("fhe_encrypt_seeded_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),

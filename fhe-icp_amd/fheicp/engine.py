@@ -86,15 +86,17 @@ class Engine:
                                                        for k in ("s_small", "s_big", "bsk", "ksk"))))
         return out
 
-    def export_fast_bsk(self) -> np.ndarray:
-        """The fast gadget's bootstrapping key (params.pbs_fast_*)."""
+    def export_fast_bsk(self, which: int = 1) -> np.ndarray:
+        """A fast gadget's bootstrapping key (which = 1: params.pbs_fast_*,
+        2: params.pbs_fast2_*)."""
         p = self.params
-        if not p.pbs_fast_level:
-            raise ValueError("these parameters have no fast gadget")
-        q = _lib.params_struct({**p.as_dict(), "pbs_base_log": p.pbs_fast_base_log,
-                                "pbs_level": p.pbs_fast_level})
+        gb, gl = ((p.pbs_fast_base_log, p.pbs_fast_level) if which == 1
+                  else (p.pbs_fast2_base_log, p.pbs_fast2_level))
+        if not gl:
+            raise ValueError(f"these parameters have no fast gadget {which}")
+        q = _lib.params_struct({**p.as_dict(), "pbs_base_log": gb, "pbs_level": gl})
         out = np.zeros(self._L.fhe_bsk_words(C.byref(q)), np.uint64)
-        self._chk(self._L.fhe_export_fast_bsk(self._ctx, C.c_void_p(out.ctypes.data)))
+        self._chk(self._L.fhe_export_fast_bsk(self._ctx, which, C.c_void_p(out.ctypes.data)))
         return out
 
     def import_keys(self, keys: dict) -> None:

@@ -37,6 +37,9 @@ class SchemeParams:
     # none (fhe_params.pbs_fast_base_log / pbs_fast_level, sign_plan())
     pbs_fast_base_log: int = 0
     pbs_fast_level: int = 0
+    # third, cheapest gadget for the last rounds (needs the fast one; 0, 0 = none)
+    pbs_fast2_base_log: int = 0
+    pbs_fast2_level: int = 0
 
     def as_dict(self) -> dict:
         return asdict(self)
@@ -82,29 +85,45 @@ def sign_rounds(P: int, d: int):
     return out
 
 
-def _plan_worst(p: "SchemeParams", d: int, j: int) -> float:
-    """Worst decision margin (sigmas) when the first j bootstraps use the main
-    gadget and the rest the fast one."""
-    v_main = _variances(p)[0]
-    v_fast = _variances(replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level))[0]
+def _gadget_var(p: "SchemeParams", g: int) -> float:
+    if g == 1 and p.pbs_fast_level:
+        return _variances(replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level))[0]
+    if g == 2 and p.pbs_fast2_level:
+        return _variances(replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level))[0]
+    return _gadget_var(p, g - 1) if g > 0 else _variances(p)[0]
+
+
+def _plan_worst(p: "SchemeParams", d: int, j1: int, j2: int | None = None) -> float:
+    """Worst decision margin (sigmas) when bootstraps [0, j1) use the main
+    gadget, [j1, j2) the fast one and the rest the fast2 one (j2 = None: all
+    the rest on the fast one)."""
+    vs = [_gadget_var(p, g) for g in range(3)]
     _, v_ks, v_ms = _variances(p)
+    rounds = sign_rounds(p.msg_bits, d)
+    if j2 is None:
+        j2 = len(rounds)
     acc, worst = 0.0, math.inf
-    for r, (sh, ml) in enumerate(sign_rounds(p.msg_bits, d)):
+    for r, (sh, ml) in enumerate(rounds):
         worst = min(worst, 2.0 ** ml / math.sqrt(acc * 4.0 ** sh + v_ks + v_ms))
-        acc += v_main if r < j else v_fast
-    return worst
+        acc += vs[0] if r < j1 else vs[1] if r < j2 else vs[2]
+    # the last bootstrap's output is the sign ciphertext: decryptable at 1/4
+    R = len(rounds)
+    v_last = vs[0] if R - 1 < j1 else vs[1] if R - 1 < j2 else vs[2]
+    return min(worst, 0.25 / math.sqrt(v_last))
 
 
 def sign_plan(p: "SchemeParams"):
-    """(d, j) of fhe_sign_batch: digit width d and how many leading bootstraps
-    use the main gadget (the rest use the fast one). Without a fast gadget: d =
-    the explicit p.sign_digit_bits, else 4 if its worst round keeps SIGMA_BAR
-    sigmas, else 3, and every round on the main gadget. With one: the widest d
-    (or the explicit one) and the fewest main-gadget rounds that keep every
-    round at SIGMA_BAR. (0, P) when P < 4 (single-bit rounds)."""
+    """(d, j1, j2) of fhe_sign_batch (fhe_sign_plan): digit width d,
+    bootstraps [0, j1) on the main gadget, [j1, j2) on the fast one, the rest
+    on the fast2 one. Without a fast gadget: d = the explicit
+    p.sign_digit_bits, else 4 if its worst round keeps SIGMA_BAR sigmas, else
+    3, and every round on the main gadget. With fast gadgets: the widest d (or
+    the explicit one), then the fewest main rounds j1 for which some j2 keeps
+    every round at SIGMA_BAR, then the fewest fast rounds (j2 = R without a
+    fast2 gadget). (0, P, P) when P < 4 (single-bit rounds)."""
     P = p.msg_bits
     if P < 4:
-        return 0, P
+        return 0, P, P
     if p.sign_digit_bits not in (0, 3, 4):
         raise ValueError("sign_digit_bits must be 0 (auto), 3 or 4")
     if not p.pbs_fast_level:
@@ -112,15 +131,23 @@ def sign_plan(p: "SchemeParams"):
             d = min(p.sign_digit_bits, P)
         else:
             d = min(4, P) if _digit_margin(p, min(4, P)) >= SIGMA_BAR else 3
-        return d, len(sign_rounds(P, d))
+        R = len(sign_rounds(P, d))
+        return d, R, R
     first = min(p.sign_digit_bits, P) if p.sign_digit_bits else min(4, P)
     last = first if p.sign_digit_bits else 3
     for d in range(first, last - 1, -1):
         R = len(sign_rounds(P, d))
-        for j in range(R + 1):
-            if _plan_worst(p, d, j) >= SIGMA_BAR:
-                return d, j
-    return last, len(sign_rounds(P, last))
+        for j1 in range(R + 1):
+            if _plan_worst(p, d, j1, R) < SIGMA_BAR:
+                continue
+            j2 = R
+            if p.pbs_fast2_level:
+                j2 = j1
+                while j2 < R and _plan_worst(p, d, j1, j2) < SIGMA_BAR:
+                    j2 += 1
+            return d, j1, j2
+    R = len(sign_rounds(P, last))
+    return last, R, R
 
 
 def sign_digit_bits(p: "SchemeParams") -> int:
@@ -131,6 +158,16 @@ def sign_digit_bits(p: "SchemeParams") -> int:
 def sign_precise_rounds(p: "SchemeParams") -> int:
     """Bootstraps of fhe_sign_batch on the main gadget (fhe_sign_precise_rounds)."""
     return sign_plan(p)[1]
+
+
+def plan_levels(p: SchemeParams) -> list:
+    """Gadget level of every bootstrap of the sign extraction, in order."""
+    P = p.msg_bits
+    if P < 4:
+        return [p.pbs_level] * max(P, 0)
+    d, j1, j2 = sign_plan(p)
+    R = len(sign_rounds(P, d))
+    return [p.pbs_level if r < j1 else p.pbs_fast_level if r < j2 else p.pbs_fast2_level for r in range(R)]
 
 
 def sign_pbs_count(p) -> int:
@@ -150,27 +187,27 @@ def sign_pbs_count(p) -> int:
 def plan_cost(p: SchemeParams) -> float:
     """Relative time of one sign extraction: its bootstraps weighted by
     BR_COST of the gadget each runs on (sign_plan)."""
-    P = p.msg_bits
-    if P < 4:
-        return P * BR_COST[p.pbs_level]
-    d, j = sign_plan(p)
-    R = len(sign_rounds(P, d))
-    return j * BR_COST[p.pbs_level] + (R - j) * BR_COST[p.pbs_fast_level or p.pbs_level]
+    return sum(BR_COST[lv] for lv in plan_levels(p))
 
 
 def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
-    """The gadget of PBS_GADGETS for width P; with fast, also the candidate
-    of FAST_GADGETS (other than the main gadget) whose sign plan is cheapest
-    by BR_COST, if it beats the single-gadget plan."""
+    """The gadget of PBS_GADGETS for width P; with fast, also up to two of
+    FAST_GADGETS (other than the main gadget, in their order: fast, then
+    fast2) for the sign rounds whose noise is barely amplified, the choice
+    whose sign plan is cheapest by BR_COST, if it beats the single-gadget
+    plan."""
     for pmax, beta, lvl in PBS_GADGETS:
         if P <= pmax:
             p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
             if fast and P >= 4:
+                cands = [g for g in FAST_GADGETS if g != (beta, lvl)]
+                choices = [(g,) for g in cands] + [(a, b) for i, a in enumerate(cands) for b in cands[i + 1:]]
                 best = plan_cost(p)
-                for fb, fl in FAST_GADGETS:
-                    if (fb, fl) == (beta, lvl):
-                        continue
-                    q = replace(p, pbs_fast_base_log=fb, pbs_fast_level=fl)
+                for ch in choices:
+                    kw = {"pbs_fast_base_log": ch[0][0], "pbs_fast_level": ch[0][1]}
+                    if len(ch) > 1:
+                        kw.update(pbs_fast2_base_log=ch[1][0], pbs_fast2_level=ch[1][1])
+                    q = replace(p, **kw)
                     c = plan_cost(q)
                     if c < best - 1e-9:
                         p, best = q, c
@@ -230,8 +267,8 @@ def noise_report(p: SchemeParams, method: str = "digits") -> dict:
     sigma = math.sqrt(v_total)
     margin_sigmas = (2.0 ** -(d + 1) if d > 1 else 0.25) / sigma
     if d > 1 and p.pbs_fast_level:
-        # two gadgets: the worst round of sign_plan's schedule
-        margin_sigmas = _plan_worst(p, d, sign_plan(p)[1])
+        # several gadgets: the worst round of sign_plan's schedule
+        margin_sigmas = _plan_worst(p, d, *sign_plan(p)[1:])
         sigma = 2.0 ** -(d + 1) / margin_sigmas
     return {
         "digit_bits": d if d > 1 else 1,

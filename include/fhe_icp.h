@@ -64,6 +64,8 @@ typedef struct fhe_params {
                                 this cheaper one. keygen makes a second
                                 bootstrapping key for it (fhe_export_fast_bsk); import
                                 re-encrypts it with fresh randomness. */
+  int32_t pbs_fast2_base_log; /* optional third, cheapest gadget (0, 0: none; needs the  */
+  int32_t pbs_fast2_level;    /* fast one): the rounds from the plan's fast_end on use it */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;
@@ -99,10 +101,11 @@ int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream);
 int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64_t* h_bsk, uint64_t* h_ksk);
 int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
                     const uint64_t* h_ksk);
-/* the fast gadget's bootstrapping key (same layout as bsk, fhe_bsk_words of
- * the params with pbs_base_log/pbs_level replaced by the fast pair; stream
- * tags 9/10). FHE_E_STATE without a fast gadget. Synchronous. */
-int fhe_export_fast_bsk(fhe_ctx* ctx, uint64_t* h_bsk2);
+/* a fast gadget's bootstrapping key, which = 1 (pbs_fast_*, stream tags
+ * 9/10) or 2 (pbs_fast2_*, tags 11/12): same layout as bsk, fhe_bsk_words of
+ * the params with pbs_base_log/pbs_level replaced by that pair. FHE_E_STATE
+ * without that gadget. Synchronous. */
+int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk);
 
 /* ---- client side: encrypt / decrypt --------------------------------------
  * Replaces the per-sample encrypt/decrypt of predict(fhe="execute")
@@ -151,6 +154,10 @@ int fhe_sign_pbs_count(const fhe_params* params);
 /* how many of them (the first ones) run on the main gadget; all of them
  * without a fast gadget */
 int fhe_sign_precise_rounds(const fhe_params* params);
+/* the whole plan: digit width, bootstraps [0, main_rounds) on the main
+ * gadget, [main_rounds, fast_end) on the fast one, the rest on fast2
+ * (DESIGN.md §3.6). Any pointer may be NULL. */
+int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_rounds, int32_t* fast_end);
 /* Bootstrap with a staircase test vector over 2^log_slots slots of the half
  * torus: output phase ~ base + floor(phase * 2^log_slots / 2^63) * step for an
  * input phase in [0, 2^63) (negacyclic beyond). log_slots = 0, step = 0 is

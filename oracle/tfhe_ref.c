@@ -47,6 +47,8 @@ typedef struct {
   int32_t sign_digit_bits; /* sign-extraction digit width, 0 = noise-model choice */
   int32_t pbs_fast_base_log; /* second (fast) bootstrap gadget for the low-  */
   int32_t pbs_fast_level;    /* amplification sign rounds; 0, 0 = none      */
+  int32_t pbs_fast2_base_log; /* third, cheapest gadget for the last rounds */
+  int32_t pbs_fast2_level;    /* (needs the fast one); 0, 0 = none          */
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -125,7 +127,8 @@ static int64_t tuniform(uint64_t w, int b) {
 int64_t ref_tuniform(uint64_t w, int b) { return tuniform(w, b); }
 
 enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, TAG_KSK_MASK = 5,
-       TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10 };
+       TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10,
+       TAG_BSK3_MASK = 11, TAG_BSK3_NOISE = 12 };
 
 /* --------------------------------------------------- negacyclic product --- */
 /* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
@@ -205,17 +208,23 @@ static void bsk_gen(const ref_params* P, const ref_key* Kp, int beta, int L, int
   }
 }
 
-/* the fast gadget's bootstrapping key (fhe_keygen with pbs_fast_*): same
- * secrets, TAG_BSK2_* streams; bsk2 has ref_bsk_words of the fast gadget */
-size_t ref_bsk2_words(const ref_params* P) {
-  return (size_t)P->n * (P->k + 1) * P->pbs_fast_level * (P->k + 1) * P->N;
+/* a fast gadget's bootstrapping key (fhe_keygen with pbs_fast_* / pbs_fast2_*):
+ * same secrets; which = 1: TAG_BSK2_* streams, 2: TAG_BSK3_*; ref_bsk2_words
+ * words (the bsk layout of that gadget) */
+size_t ref_bsk2_words(const ref_params* P, int which) {
+  const int L = which == 1 ? P->pbs_fast_level : P->pbs_fast2_level;
+  return (size_t)P->n * (P->k + 1) * L * (P->k + 1) * P->N;
 }
-int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, const uint64_t* s_small, const uint64_t* s_big,
-                        uint64_t* bsk2) {
-  if (!P->pbs_fast_level) return -1;
+int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uint64_t* s_small,
+                        const uint64_t* s_big, uint64_t* bsk2) {
+  const int L = which == 1 ? P->pbs_fast_level : which == 2 ? P->pbs_fast2_level : 0;
+  if (!L) return -1;
   ref_key K;
   key_from_seed(seed, &K);
-  bsk_gen(P, &K, P->pbs_fast_base_log, P->pbs_fast_level, TAG_BSK2_MASK, TAG_BSK2_NOISE, s_small, s_big, bsk2);
+  if (which == 1)
+    bsk_gen(P, &K, P->pbs_fast_base_log, L, TAG_BSK2_MASK, TAG_BSK2_NOISE, s_small, s_big, bsk2);
+  else
+    bsk_gen(P, &K, P->pbs_fast2_base_log, L, TAG_BSK3_MASK, TAG_BSK3_NOISE, s_small, s_big, bsk2);
   return 0;
 }
 
@@ -599,24 +608,30 @@ static int plan_rounds(int Pb, int d, int* shift, int* mlog) {
   shift[R] = 0; mlog[R++] = -(d + 1);
   return R;
 }
-static double plan_margin(const ref_params* P, int d, int j) {
+static double plan_margin(const ref_params* P, int d, int j1, int j2) {
   int sh[64], ml[64];
   const int R = plan_rounds(P->msg_bits, d, sh, ml);
   const double vm = pbs_variance(P, P->pbs_base_log, P->pbs_level);
   const double vf = P->pbs_fast_level ? pbs_variance(P, P->pbs_fast_base_log, P->pbs_fast_level) : vm;
+  const double vf2 = P->pbs_fast2_level ? pbs_variance(P, P->pbs_fast2_base_log, P->pbs_fast2_level) : vf;
   const double fx = fixed_variance(P);
   double acc = 0, worst = INFINITY;
   for (int r = 0; r < R; ++r) {
     const double m = ldexp(1.0, ml[r]) / sqrt(acc * ldexp(1.0, 2 * sh[r]) + fx);
     if (m < worst) worst = m;
-    acc += r < j ? vm : vf;
+    acc += r < j1 ? vm : r < j2 ? vf : vf2;
   }
-  return worst;
+  /* the last bootstrap's output is the sign ciphertext: decryptable at 1/4 */
+  const double vl = R - 1 < j1 ? vm : R - 1 < j2 ? vf : vf2;
+  const double ml_last = 0.25 / sqrt(vl);
+  return ml_last < worst ? ml_last : worst;
 }
-static void sign_plan(const ref_params* P, int* d_out, int* j_out) {
+/* (d, j1, j2): bootstraps [0, j1) on the main gadget, [j1, j2) on the fast
+ * one, the rest on fast2 */
+static void sign_plan(const ref_params* P, int* d_out, int* j1_out, int* j2_out) {
   int sh[64], ml[64];
   const int Pb = P->msg_bits, d4 = Pb < 4 ? Pb : 4;
-  if (Pb < 4) { *d_out = 0; *j_out = Pb; return; }
+  if (Pb < 4) { *d_out = 0; *j1_out = *j2_out = Pb; return; }
   if (!P->pbs_fast_level) {
     int d = 3;
     if (P->sign_digit_bits) {
@@ -629,36 +644,46 @@ static void sign_plan(const ref_params* P, int* d_out, int* j_out) {
       if (ldexp(1.0, -(d4 + 1)) / sqrt(v) >= 9.2) d = d4;
     }
     *d_out = d;
-    *j_out = plan_rounds(Pb, d, sh, ml);
+    *j1_out = *j2_out = plan_rounds(Pb, d, sh, ml);
     return;
   }
   const int first = P->sign_digit_bits ? (P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb) : d4;
   const int last = P->sign_digit_bits ? first : 3;
   for (int d = first; d >= last; --d) {
     const int R = plan_rounds(Pb, d, sh, ml);
-    for (int j = 0; j <= R; ++j)
-      if (plan_margin(P, d, j) >= 9.2) { *d_out = d; *j_out = j; return; }
+    for (int j1 = 0; j1 <= R; ++j1) {
+      if (plan_margin(P, d, j1, R) < 9.2) continue;
+      int j2 = R;
+      if (P->pbs_fast2_level) {
+        j2 = j1;
+        while (j2 < R && plan_margin(P, d, j1, j2) < 9.2) ++j2;
+      }
+      *d_out = d; *j1_out = j1; *j2_out = j2;
+      return;
+    }
   }
   *d_out = last;
-  *j_out = plan_rounds(Pb, last, sh, ml);
+  *j1_out = *j2_out = plan_rounds(Pb, last, sh, ml);
 }
 static int digit_bits(const ref_params* P) {
-  int d, j;
-  sign_plan(P, &d, &j);
+  int d, j1, j2;
+  sign_plan(P, &d, &j1, &j2);
   return d;
 }
 
-/* the bootstrap gadget and key of round r: the main one for r < j, else the fast one */
+/* the bootstrap gadget and key of round r: main for r < j1, fast for r < j2,
+ * else fast2 */
 typedef struct {
   const ref_params* P;
-  ref_params Pf; /* P seen through the fast gadget */
-  const uint64_t *bsk, *bsk2;
-  int j, r;
+  ref_params Pf[2]; /* P seen through the fast / fast2 gadget */
+  const uint64_t* bsk[3];
+  int j1, j2, r;
 } gadget_sched;
 static void sched_next(gadget_sched* g, const ref_params** Pr, const uint64_t** bk) {
-  const int fast = g->bsk2 && g->r++ >= g->j;
-  *Pr = fast ? &g->Pf : g->P;
-  *bk = fast ? g->bsk2 : g->bsk;
+  const int r = g->r++;
+  const int gi = r < g->j1 ? 0 : r < g->j2 ? 1 : 2;
+  *Pr = gi ? &g->Pf[gi - 1] : g->P;
+  *bk = g->bsk[gi];
 }
 
 /* One c-bit digit [b, b+c) of the value in cv: a sign bootstrap of its top bit
@@ -682,20 +707,23 @@ static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int
  * digits [b, b+d) by digit_rounds, a leftover of >= 3 bits as one shorter
  * digit, of 1-2 bits by single-bit rounds; then the sign of the top d bits
  * (centred by 2^(63-d), tv 2^62). sign[count x (kN+1)] encrypts [v < 0] at
- * 2^63; ct_v is consumed. With a fast gadget (P->pbs_fast_*) and its key bsk2,
- * bootstraps from the j-th on (sign_plan) use it; bsk2 = NULL plans as if no
- * fast gadget were set. */
-void ref_sign_extract2(const ref_params* P0, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* ksk,
-                       uint64_t* ct_v, int64_t count, uint64_t* sign) {
+ * 2^63; ct_v is consumed. With fast gadgets (P->pbs_fast_*, P->pbs_fast2_*) and
+ * their keys bsk2, bsk3, bootstraps [j1, j2) of sign_plan use the fast one and
+ * the rest the fast2 one; a NULL key plans as if that gadget were not set. */
+void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* bsk3,
+                       const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
   ref_params Pm = *P0;
   if (!bsk2) Pm.pbs_fast_base_log = Pm.pbs_fast_level = 0;
+  if (!bsk2 || !bsk3) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = 0;
   const ref_params* P = &Pm;
   const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
-  int d, j;
-  sign_plan(P, &d, &j);
-  ref_params Pf = *P;
-  if (P->pbs_fast_level) { Pf.pbs_base_log = P->pbs_fast_base_log; Pf.pbs_level = P->pbs_fast_level; }
-  const size_t ww = pbs_work_words(P) > pbs_work_words(&Pf) ? pbs_work_words(P) : pbs_work_words(&Pf);
+  int d, j1, j2;
+  sign_plan(P, &d, &j1, &j2);
+  ref_params Pf[2] = {*P, *P};
+  if (P->pbs_fast_level) { Pf[0].pbs_base_log = P->pbs_fast_base_log; Pf[0].pbs_level = P->pbs_fast_level; }
+  if (P->pbs_fast2_level) { Pf[1].pbs_base_log = P->pbs_fast2_base_log; Pf[1].pbs_level = P->pbs_fast2_level; }
+  size_t ww = pbs_work_words(P);
+  for (int g = 0; g < 2; ++g) if (pbs_work_words(&Pf[g]) > ww) ww = pbs_work_words(&Pf[g]);
 #pragma omp parallel
   {
     uint64_t* work = (uint64_t*)malloc(8 * ww);
@@ -705,7 +733,7 @@ void ref_sign_extract2(const ref_params* P0, const uint64_t* bsk, const uint64_t
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c) {
       uint64_t* cv = ct_v + (size_t)c * Wb;
-      gadget_sched g = {P, Pf, bsk, P->pbs_fast_level ? bsk2 : NULL, j, 0};
+      gadget_sched g = {P, {Pf[0], Pf[1]}, {bsk, bsk2, bsk3}, j1, j2, 0};
       const ref_params* Pr;
       const uint64_t* bk;
       if (Pb < 4) {
@@ -737,13 +765,18 @@ void ref_sign_extract2(const ref_params* P0, const uint64_t* bsk, const uint64_t
 }
 void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
                       uint64_t* sign) {
-  ref_sign_extract2(P, bsk, NULL, ksk, ct_v, count, sign);
+  ref_sign_extract3(P, bsk, NULL, NULL, ksk, ct_v, count, sign);
 }
 
 int ref_sign_precise_rounds(const ref_params* P) {
-  int d, j;
-  sign_plan(P, &d, &j);
-  return j;
+  int d, j1, j2;
+  sign_plan(P, &d, &j1, &j2);
+  return j1;
+}
+void ref_sign_plan(const ref_params* P, int32_t* d, int32_t* j1, int32_t* j2) {
+  int a, b, c;
+  sign_plan(P, &a, &b, &c);
+  *d = a; *j1 = b; *j2 = c;
 }
 
 int ref_sign_digit_bits(const ref_params* P) { return digit_bits(P); }

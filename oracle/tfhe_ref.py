@@ -17,8 +17,8 @@ _LIB_PATH = _HERE / "build" / "libtfhe_ref.so"
 
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
           "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
-          "pbs_fast_base_log", "pbs_fast_level")
-OPTIONAL = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level")
+          "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level")
+OPTIONAL = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level")
 
 
 class RefParams(C.Structure):
@@ -59,10 +59,11 @@ def lib():
         L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
         L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
-        L.ref_sign_extract2.argtypes = [P, u64p, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_extract3.argtypes = [P, u64p, u64p, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_plan.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.ref_sign_precise_rounds.argtypes = [P]; L.ref_sign_precise_rounds.restype = C.c_int
-        L.ref_bsk2_words.argtypes = [P]; L.ref_bsk2_words.restype = C.c_size_t
-        L.ref_keygen_fast_bsk.argtypes = [P, C.c_uint64, u64p, u64p, u64p]
+        L.ref_bsk2_words.argtypes = [P, C.c_int]; L.ref_bsk2_words.restype = C.c_size_t
+        L.ref_keygen_fast_bsk.argtypes = [P, C.c_uint64, C.c_int, u64p, u64p, u64p]
         L.ref_sign_pbs_count.argtypes = [P]; L.ref_sign_pbs_count.restype = C.c_int
         L.ref_sign_digit_bits.argtypes = [P]; L.ref_sign_digit_bits.restype = C.c_int
         L.ref_negacyclic_mul.argtypes = [u64p, u64p, u64p, C.c_int]
@@ -104,12 +105,17 @@ class RefTFHE:
         self.ksk = np.zeros(L.ref_ksk_words(C.byref(self.P)), np.uint64)
         L.ref_keygen(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big), u64(self.bsk),
                      u64(self.ksk))
-        # the fast gadget's bootstrapping key (fhe_keygen generates it too)
-        self.bsk2 = None
-        if self.params["pbs_fast_level"]:
-            self.bsk2 = np.zeros(L.ref_bsk2_words(C.byref(self.P)), np.uint64)
-            L.ref_keygen_fast_bsk(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big),
-                                  u64(self.bsk2))
+        # the fast gadgets' bootstrapping keys (fhe_keygen generates them too)
+        self.bsk2 = self.bsk3 = None
+        for which, lv in ((1, "pbs_fast_level"), (2, "pbs_fast2_level")):
+            if self.params[lv]:
+                b = np.zeros(L.ref_bsk2_words(C.byref(self.P), which), np.uint64)
+                L.ref_keygen_fast_bsk(C.byref(self.P), C.c_uint64(seed), which, u64(self.s_small), u64(self.s_big),
+                                      u64(b))
+                if which == 1:
+                    self.bsk2 = b
+                else:
+                    self.bsk3 = b
 
     def with_msg_bits(self, P: int) -> "RefTFHE":
         self.params["msg_bits"] = int(P)
@@ -214,7 +220,8 @@ class RefTFHE:
         cnt = cv.size // (self.big + 1)
         sign = np.zeros((cnt, self.big + 1), np.uint64)
         bsk2 = u64(self.bsk2) if self.bsk2 is not None else None
-        lib().ref_sign_extract2(C.byref(self.P), u64(self.bsk), bsk2, u64(self.ksk), u64(cv), cnt, u64(sign))
+        bsk3 = u64(self.bsk3) if self.bsk3 is not None else None
+        lib().ref_sign_extract3(C.byref(self.P), u64(self.bsk), bsk2, bsk3, u64(self.ksk), u64(cv), cnt, u64(sign))
         return sign
 
     def bit_extract(self, ct_v: np.ndarray):
@@ -272,3 +279,9 @@ def sign_pbs_count(params: dict) -> int:
 
 def sign_precise_rounds(params: dict) -> int:
     return int(lib().ref_sign_precise_rounds(C.byref(_ref_params(params))))
+
+
+def sign_plan(params: dict):
+    d, j1, j2 = C.c_int32(), C.c_int32(), C.c_int32()
+    lib().ref_sign_plan(C.byref(_ref_params(params)), C.byref(d), C.byref(j1), C.byref(j2))
+    return d.value, j1.value, j2.value

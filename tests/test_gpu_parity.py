@@ -218,15 +218,17 @@ TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_leve
 @pytest.mark.parametrize("P", [8, 16, 19])
 def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P):
     """Both bootstrapping keys of a two-gadget parameter set (toy (12,3)+(8,2);
-    real P=16: (15,2)+(23,1); P=19: (12,3)+(15,2)) are bit-exact against the
-    oracle's keygen."""
+    real P=16: (15,2)+(23,1); P=19: (12,3)+(15,2)+(23,1)) are bit-exact
+    against the oracle's keygen."""
     prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 12 else params_for_bits(P)
     assert prm.pbs_fast_level
     eng = Engine(prm, 0)
     eng.keygen(4321)
     ref = oracle_lib.RefTFHE(prm.as_dict(), 4321)
     assert np.array_equal(eng.export_keys()["bsk"], ref.bsk)
-    assert np.array_equal(eng.export_fast_bsk(), ref.bsk2)
+    assert np.array_equal(eng.export_fast_bsk(1), ref.bsk2)
+    if prm.pbs_fast2_level:
+        assert np.array_equal(eng.export_fast_bsk(2), ref.bsk3)
     eng.close()
 
 
@@ -237,7 +239,7 @@ def test_sign_toy_fast_gadget_vs_oracle(need_gpu, oracle_lib, P, dbits):
     ciphertexts' phases track the oracle's two-key restatement."""
     from fheicp.params import sign_plan, sign_rounds
     prm = replace(TOY, msg_bits=P, sign_digit_bits=dbits, **TOY_FAST)
-    d, j = sign_plan(prm)
+    d, j, _ = sign_plan(prm)
     assert 0 < j < len(sign_rounds(P, d))
     eng = Engine(prm, 0)
     eng.keygen(4321)
@@ -262,6 +264,37 @@ def test_sign_toy_fast_gadget_vs_oracle(need_gpu, oracle_lib, P, dbits):
     eng.close()
 
 
+TOY_FAST3 = dict(TOY_FAST, pbs_fast2_base_log=11, pbs_fast2_level=1)
+
+
+@pytest.mark.parametrize("P,dbits", [(8, 3), (11, 4)])
+def test_sign_toy_three_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits):
+    """Three gadgets (toy (12,3) + (8,2) + (11,1)): the plan puts rounds on
+    all three keys; every value is exact and the phases track the oracle."""
+    from fheicp.params import sign_plan, sign_rounds
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=dbits, **TOY_FAST3)
+    d, j1, j2 = sign_plan(prm)
+    assert 0 < j1 < j2 < len(sign_rounds(P, d))
+    eng = Engine(prm, 0)
+    eng.keygen(4323)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 4323)
+    assert np.array_equal(eng.export_fast_bsk(2), ref.bsk3)
+    v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
+    sign = eng.sign(eng.encrypt(v, seed=63))
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    h = 2 ** (P - 1)
+    sel = np.array([0, 1, h - 1, h, h + 1, 2 * h - 1])
+    s_ref = ref.sign_extract(ref.encrypt_ints(v[sel], seed=63, id0=0))
+    assert np.array_equal(ref.decrypt_bits(s_ref), (v[sel] < 0).astype(np.int64))
+    # the last round runs on the coarse (11,1) toy gadget: the two outputs'
+    # noise (sigma ~2^58) differs wherever a rounding decision of the gadget
+    # decomposition flips, so they agree within the noise, inside the 2^62
+    # decryption margin
+    dph = signed(u64(eng.phase(sign[sel].contiguous())) - ref.phase(s_ref))
+    assert np.abs(dph).max() < 2 ** 61
+    eng.close()
+
+
 @pytest.mark.parametrize("P,dbits,fast", [(16, 0, True), (16, 3, True), (19, 0, True), (19, 0, False),
                                           (21, 0, True), (21, 0, False)])
 def test_sign_real_params(need_gpu, P, dbits, fast):
@@ -277,6 +310,26 @@ def test_sign_real_params(need_gpu, P, dbits, fast):
     sign = eng.sign(eng.encrypt(v, seed=P))
     assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
     eng.close()
+
+
+def test_sign_every_width(need_gpu):
+    """Every accumulator width the parameter table supports (P = 2..27), each
+    with its params_for_bits gadgets and sign plan (single gadget, (23,1) or
+    (15,2) fast rounds; v4 32- and 64-bit and v2 kernels): the boundary values
+    and a random sample keep their exact sign."""
+    from fheicp.params import sign_plan
+    rng = np.random.default_rng(2027)
+    for P in range(2, 28):
+        prm = params_for_bits(P)
+        eng = Engine(prm, 0)
+        eng.keygen(3000 + P)
+        h = 2 ** (P - 1)
+        v = np.concatenate([[-h, -h + 1, -2, -1, 0, 1, h - 2, h - 1] if P > 2 else [-2, -1, 0, 1],
+                            rng.integers(-h, h, 248)]).astype(np.int64)
+        sign = eng.sign(eng.encrypt(v, seed=P))
+        got = eng.decrypt_bits(sign).cpu().numpy()
+        assert np.array_equal(got, (v < 0).astype(np.int64)), (P, sign_plan(prm))
+        eng.close()
 
 
 def test_pbs_lut_real_vs_oracle(real):

@@ -174,7 +174,7 @@ def test_sign_extract_fast_gadget_values(oracle_lib, P, d):
     from dataclasses import replace
     from fheicp.params import TOY, sign_plan, sign_rounds
     prm = replace(TOY, msg_bits=P, sign_digit_bits=d, **TOY_FAST)
-    dd, j = sign_plan(prm)
+    dd, j, _ = sign_plan(prm)
     assert dd == d and (j < len(sign_rounds(P, d)) or P == 5)
     r = oracle_lib.RefTFHE(prm.as_dict(), 4321)
     assert r.bsk2 is not None and oracle_lib.sign_precise_rounds(prm.as_dict()) == j
@@ -184,4 +184,28 @@ def test_sign_extract_fast_gadget_values(oracle_lib, P, d):
         v = np.concatenate([[-h, -h + 1, -2, -1, 0, 1, h - 2, h - 1],
                             np.random.default_rng(P).integers(-h, h, 120)]).astype(np.int64)
     sign = r.sign_extract(r.encrypt_ints(v, seed=200 + P))
+    assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
+
+
+TOY_FAST3 = {"pbs_base_log": 12, "pbs_level": 3, "pbs_fast_base_log": 8, "pbs_fast_level": 2,
+             "pbs_fast2_base_log": 11, "pbs_fast2_level": 1}
+
+
+@pytest.mark.parametrize("P,d", [(8, 3), (11, 4)])
+def test_sign_extract_three_gadgets(oracle_lib, P, d):
+    """Three gadgets on a toy set whose fast (8,2) and fast2 (11,1) gadgets are
+    coarse enough that the plan uses all three keys; the values keep their
+    sign and the plan matches the library's."""
+    from dataclasses import replace
+    from fheicp.params import TOY, sign_plan, sign_rounds
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=d, **TOY_FAST3)
+    dd, j1, j2 = sign_plan(prm)
+    assert dd == d and 0 < j1 < j2 < len(sign_rounds(P, d)), (j1, j2)
+    assert oracle_lib.sign_plan(prm.as_dict()) == (dd, j1, j2)
+    r = oracle_lib.RefTFHE(prm.as_dict(), 4322)
+    assert r.bsk2 is not None and r.bsk3 is not None
+    h = 2 ** (P - 1)
+    v = np.concatenate([[-h, -h + 1, -2, -1, 0, 1, h - 2, h - 1],
+                        np.random.default_rng(P).integers(-h, h, 120)]).astype(np.int64)
+    sign = r.sign_extract(r.encrypt_ints(v, seed=300 + P))
     assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))

@@ -32,6 +32,10 @@ def _param_sets():
     for P in range(2, 28):
         for fast in (True, False):
             p = params_for_bits(P, fast=fast)
+            if fast and p.pbs_fast2_level:   # also the two-gadget variant
+                q = p.__class__(**{**p.as_dict(), "pbs_fast2_base_log": 0, "pbs_fast2_level": 0})
+                for d in (0, 3, 4):
+                    yield q.__class__(**{**q.as_dict(), "sign_digit_bits": d})
             for d in (0, 3, 4):
                 yield p.with_msg_bits(P).__class__(**{**p.as_dict(), "sign_digit_bits": d})
     for P in range(2, 17):
@@ -49,6 +53,10 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
         assert sign_digit_bits(p) == oracle_lib.sign_digit_bits(d) == L.fhe_sign_digit_bits(cp), d
         assert sign_pbs_count(p) == oracle_lib.sign_pbs_count(d) == L.fhe_sign_pbs_count(cp), d
         assert sign_precise_rounds(p) == oracle_lib.sign_precise_rounds(d) == L.fhe_sign_precise_rounds(cp), d
+        import ctypes as C
+        dd, j1, j2 = C.c_int32(), C.c_int32(), C.c_int32()
+        assert L.fhe_sign_plan(cp, C.byref(dd), C.byref(j1), C.byref(j2)) == 0
+        assert sign_plan(p) == oracle_lib.sign_plan(d) == (dd.value, j1.value, j2.value), d
     # the headline width: 4-bit digits at P = 16, 3-bit where 4 misses the bar
     assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 3, 3, 3]
     assert sign_pbs_count(16) == 7
@@ -57,25 +65,31 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
 
 def test_fast_gadget_plan():
     """Per-round gadgets: params_for_bits adds the cheapest
-    fast gadget (by BR_COST) for the sign rounds whose noise is barely
+    set of fast gadgets (by BR_COST) for the sign rounds whose noise is barely
     amplified; only the leading rounds, whose output is shifted up the most,
-    stay on the precise gadget, and every round keeps 9.2 sigma."""
+    stay on the precise gadget, and every round keeps 9.2 sigma with the
+    fewest main, then fast, rounds."""
     from fheicp.params import _plan_worst, plan_cost
-    want = {4: ((23, 1), 4, 0), 9: ((23, 1), 4, 0), 12: ((23, 1), 4, 1), 16: ((23, 1), 4, 3),
-            17: ((23, 1), 3, 5), 18: ((15, 2), 4, 1), 19: ((15, 2), 4, 1), 20: ((15, 2), 4, 2),
-            21: ((15, 2), 3, 3), 22: ((15, 2), 4, 3), 23: ((15, 2), 3, 4), 24: ((15, 2), 4, 4),
-            25: ((15, 2), 3, 5), 26: ((15, 2), 3, 6), 27: ((15, 2), 3, 7)}
-    for P, (fg, d, j) in want.items():
+    F, F2 = (15, 2), (23, 1)
+    want = {4: (F2, None, (4, 0, 1)), 9: (F2, None, (4, 0, 4)), 12: (F2, None, (4, 1, 5)),
+            16: (F2, None, (4, 3, 7)), 17: (F2, None, (3, 5, 11)), 18: (F, F2, (4, 1, 5)),
+            19: (F, F2, (4, 1, 5)), 20: (F, F2, (4, 2, 5)), 21: (F, F2, (3, 3, 7)), 22: (F, F2, (4, 3, 7)),
+            23: (F, F2, (3, 4, 9)), 24: (F, F2, (4, 4, 7)), 25: (F, F2, (3, 5, 10)), 26: (F, F2, (3, 6, 11)),
+            27: (F, F2, (3, 7, 11))}
+    for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
         assert (p.pbs_fast_base_log, p.pbs_fast_level) == fg, P
-        assert sign_plan(p) == (d, j), P
-        assert _plan_worst(p, d, j) >= 9.2
-        assert j == 0 or _plan_worst(p, d, j - 1) < 9.2
-        assert len(sign_rounds(P, d)) == sign_pbs_count(p)
+        assert ((p.pbs_fast2_base_log, p.pbs_fast2_level) if p.pbs_fast2_level else None) == fg2, P
+        R = len(sign_rounds(P, d))
+        assert sign_plan(p) == (d, j1, j2 if fg2 else R), P
+        assert _plan_worst(p, d, j1, j2) >= 9.2
+        assert j1 == 0 or _plan_worst(p, d, j1 - 1, R) < 9.2
+        assert fg2 is None or j2 == j1 or _plan_worst(p, d, j1, j2 - 1) < 9.2
+        assert R == sign_pbs_count(p)
         assert plan_cost(p) < plan_cost(params_for_bits(P, fast=False))
     # the headline width keeps its 4-bit digits and the single-gadget worst round
-    assert sign_plan(params_for_bits(16)) == (4, 3)
-    assert sign_plan(params_for_bits(19, fast=False)) == (4, 9)
+    assert sign_plan(params_for_bits(16)) == (4, 3, 7)
+    assert sign_plan(params_for_bits(19, fast=False)) == (4, 9, 9)
     assert params_for_bits(3).pbs_fast_level == 0
 
 
