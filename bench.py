@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--min-similarity", type=float, default=0.5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-compares", type=int, default=32)
+    ap.add_argument("--cpu-compares", type=int, default=0,
+                    help="oracle sample size (0: 32 compares scaled down by the sign plan's cost, 10-30 s)")
     ap.add_argument("--mode", choices=("compare", "corpus"), default="compare",
                     help="compare: the reference's path (configs[1]); corpus: search over a stored corpus of "
                          "seeded-LWE documents (SURVEY.md §8f-1)")
@@ -152,7 +153,7 @@ def roofline(p, brs) -> dict:
             tr = json.loads(tj.read_text())
             q = qs[dom]
             if (tr.get("pbs_level"), tr.get("pbs_base_log", q.pbs_base_log)) == (q.pbs_level, q.pbs_base_log) \
-                    and tr.get("kernel_build") == TRAFFIC_BUILD:
+                    and tr.get("kernel_build") == TRAFFIC_BUILD and tr.get("cts_per_launch") == k["cts_per_launch"]:
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -298,6 +299,16 @@ def topk_check(args, model, world, oa, oi):
             "scores_equal": got_scores == [sc_ for _, sc_ in keep[:args.top_k]]}
 
 
+def cpu_sample(args, p) -> int:
+    """Compares timed on the CPU oracle: --cpu-compares, or 32 at the
+    headline's plan cost (5.6 relative bootstraps, about 11 s on 16 host
+    threads) scaled down to the configuration's plan, at least 8."""
+    if args.cpu_compares:
+        return args.cpu_compares
+    from fheicp.params import plan_cost
+    return int(max(8, min(32, round(32 * 5.6 / max(plan_cost(p), 1e-9)))))
+
+
 def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
     """The oracle, timed on the host cores (bounded sample), and the parity
     check of the last timed step against the clear restatement."""
@@ -320,7 +331,7 @@ def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
     # decrypt + the digit sign extraction (all its KS + PBS) + decrypt.
     p = model.engine.params.as_dict()
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    C = args.cpu_compares
+    C = cpu_sample(args, model.engine.params)
     ref = R.RefTFHE(p, args.seed)
     qx = Q.quantize_input(oq, Xp[:C])
     t0 = time.perf_counter()
@@ -454,10 +465,10 @@ def corpus_cpu_leg(args, c, bodies, ids, oq, cq, q_np, docs_np, P, parity):
     the seeded documents, linear, decrypt, sign extraction, decrypt."""
     from oracle import quant_ref as Q
     from oracle import tfhe_ref as R
-    Cn = args.cpu_compares
     p0 = c.scheme.as_dict()
     ref = R.RefTFHE(p0, args.seed)
     Wr, cst, T, P = c.query_plan(q_np, args.min_similarity)
+    Cn = cpu_sample(args, c.scheme.with_msg_bits(P))
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     t0 = time.perf_counter()
     ct = ref.expand_seeded(bodies[:Cn], ids[:Cn], c.mask_key)
