@@ -466,6 +466,20 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
 #pragma unroll
         for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gpo[u * 64 + lane];
       }
+      // the 32-bit-accumulator kernels also start one of the two other rows'
+      // loads before the transform, at the first level (the MAC accumulator
+      // is not live yet): 7.78 -> 7.02 ms per 1024 bootstraps at (23,1) (166
+      // VGPRs), 11.92 -> 11.11 ms at (15,2) (168 VGPRs and a 20-byte spill;
+      // loading only half the row early, without the spill, measured the same)
+      constexpr bool EARLY_CT = A32 && PF;
+      const bool EARLY = EARLY_CT && lv == 0;
+      c64 ke[EARLY_CT ? S : 1];
+      if (EARLY_CT && EARLY) {
+        const int cin = comp + 1 >= WPC ? comp + 1 - WPC : comp + 1;
+        const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
+#pragma unroll
+        for (int u = 0; u < S; ++u) ke[u] = (DBG & 2) ? c64{wf.x, wf.y + u} : gp[u * 64 + lane];
+      }
       // FL: the others must have read this slot's previous F before the
       // transform's relayouts overwrite it
       if constexpr (FL && (DBG & 4) == 0)
@@ -492,7 +506,10 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
           const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
           const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
 #pragma unroll
-          for (int u = 0; u < S; ++u) kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
+          for (int u = 0; u < S; ++u) {
+            if (EARLY && ci == 0) kx[ci][u] = ke[u];
+            else kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
+          }
         }
       }
       V4_STAMP(3 + 5 * lv);
