@@ -314,8 +314,8 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
 
 static void free_ev(ProfAcc& a) {
   for (auto& e : a.ev) {
-    hipEventDestroy(e.first);
-    hipEventDestroy(e.second);
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
   }
   a.ev.clear();
 }
@@ -323,11 +323,13 @@ static void free_ev(ProfAcc& a) {
 void fhe_ctx_destroy(fhe_ctx* ctx) {
   if (!ctx) return;
   if (ctx->device >= 0) {
-    hipSetDevice(ctx->device);
-    hipFree(ctx->s_small); hipFree(ctx->s_big); hipFree(ctx->bsk); hipFree(ctx->ksk); hipFree(ctx->ksk_colsum);
-    hipFree(ctx->bsk_fft); hipFree(ctx->tw); hipFree(ctx->twist); hipFree(ctx->ws);
-    for (int g = 0; g < 2; ++g) hipFree(ctx->bskf[g]), hipFree(ctx->bskf_fft[g]);
-    hipFree(ctx->ksk8); hipFree(ctx->ks_ws); hipFree(ctx->tw4);
+    // teardown: nothing useful can be done about a failed free
+    (void)hipSetDevice(ctx->device);
+    for (void* ptr : {(void*)ctx->s_small, (void*)ctx->s_big, (void*)ctx->bsk, (void*)ctx->ksk,
+                      (void*)ctx->ksk_colsum, (void*)ctx->bsk_fft, (void*)ctx->tw, (void*)ctx->twist, ctx->ws,
+                      (void*)ctx->bskf[0], (void*)ctx->bskf[1], (void*)ctx->bskf_fft[0], (void*)ctx->bskf_fft[1],
+                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4})
+      (void)hipFree(ptr);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_brf[0]);
     free_ev(ctx->prof_brf[1]);
@@ -641,14 +643,18 @@ static void prof_begin(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t* e1)
   *e1 = nullptr;
   if (!ctx->prof) return;
   hipEvent_t e0;
-  hipEventCreate(&e0);
-  hipEventCreate(e1);
-  hipEventRecord(e0, st);
+  if (hipEventCreate(&e0) != hipSuccess) return;
+  if (hipEventCreate(e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    *e1 = nullptr;
+    return;
+  }
+  (void)hipEventRecord(e0, st);  // a failed record shows up in fhe_profile_read
   a.ev.push_back({e0, *e1});
 }
 static void prof_end(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t e1, int64_t items) {
   if (!ctx->prof || !e1) return;
-  hipEventRecord(e1, st);
+  (void)hipEventRecord(e1, st);
   a.launches += 1;
   a.items += items;
 }
