@@ -72,3 +72,27 @@ def test_engine_refuses_without_gpu():
     from fheicp.engine import Engine
     with pytest.raises(_lib.FheError):
         Engine(TOY, 0)
+
+
+def test_fast_gadget_validation_and_host_calls():
+    """The fast-gadget fields: a fast2 gadget needs a fast one, each pair is
+    all-or-nothing; fhe_sign_plan tolerates NULL outputs; a host-only context
+    refuses to export a fast key."""
+    L = _lib.lib()
+    h = C.c_void_p()
+    base = params_for_bits(19).as_dict()
+    for bad, why in ((dict(base, pbs_fast_base_log=0, pbs_fast_level=0), b"fast2"),
+                     (dict(base, pbs_fast2_level=0), b"fast2"),
+                     (dict(base, pbs_fast_level=0), b"fast pbs")):
+        P = _lib.params_struct(bad)
+        assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1, bad
+        assert why in L.fhe_last_error(None), L.fhe_last_error(None)
+        assert L.fhe_sign_plan(C.byref(P), None, None, None) == -1
+    P = _lib.params_struct(base)
+    assert L.fhe_sign_plan(C.byref(P), None, None, None) == 0
+    j1 = C.c_int32()
+    assert L.fhe_sign_plan(C.byref(P), None, C.byref(j1), None) == 0 and j1.value == 1
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
+    buf = (C.c_uint64 * 1)()
+    assert L.fhe_export_fast_bsk(h, 1, buf) == -2
+    L.fhe_ctx_destroy(h)
