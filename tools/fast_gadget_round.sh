@@ -1,3 +1,4 @@
+# GPU check of the per-round gadget change: its parity tests, then the C3, C5 and corpus benches
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -k "fast or sign_real or keygen or sign_toy" > gpurun_out/fast_tests.log 2>&1 || { tail -30 gpurun_out/fast_tests.log; exit 1; }

@@ -1,3 +1,4 @@
+# GPU check of the exact 32-bit accumulator rounding: noise and time per gadget, 64-bit comparison, all GPU tests, the headline bench
 mkdir -p gpurun_out
 GADGETS="15,2 23,1 22,1 21,1" bash tools/ab_gadgets.sh > gpurun_out/ab_gadgets2.log 2>&1 || { cat gpurun_out/ab_gadgets2.log; exit 1; }
 FHEICP_V4_G=2 FHEICP_V4_A64=1 timeout -k 10 120 python tools/prof_br.py --variants 4 --rounds 2 --P 16 >> gpurun_out/ab_gadgets2.log 2>&1 || exit 1
