@@ -35,9 +35,11 @@ import torch  # noqa: E402
 
 METRIC = "encrypted compares/sec (PBS/sec), 16-dim, 1/2/4/8 GPU; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
-# kernel build the committed PMC traffic (profiles/r01_br_traffic.json) was measured on
-TRAFFIC_BUILD = "v4-a32-exact-round"
-F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector peak (spec)
+F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector peak (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
+# PMC measurement of this build's blind-rotation kernels (tools/pmc_bench.sh ->
+# tools/br_pmc.py): executed f64 FLOPs and HBM bytes per launch, keyed on the
+# sha256 of the libfheicp.so they were measured on
+PMC_FILE = REPO / "profiles" / "br_pmc.json"
 
 
 def parse():
@@ -100,7 +102,8 @@ def config_tag(args) -> str:
 
 
 def br_flops_per_ct(p) -> float:
-    """Analytic f64 FLOPs of one blind rotation."""
+    """Analytic f64 FLOPs of one blind rotation (radix-2 FFT count, DESIGN.md
+    §4.2); used only when no PMC measurement of this build exists."""
     M = p.N // 2
     logm = int(np.log2(M))
     fft = 5.0 * M * logm + 6.0 * M             # radix-2 complex FFT + twist
@@ -109,70 +112,102 @@ def br_flops_per_ct(p) -> float:
     return p.n * (nf * fft + ni * fft + pointwise)
 
 
+def lib_sha256() -> str:
+    import hashlib
+    from fheicp import _lib
+    return hashlib.sha256(Path(_lib.LIB_PATH).read_bytes()).hexdigest()
+
+
+def load_pmc() -> dict:
+    """Per-kernel PMC figures of THIS build ({} if the file was measured on
+    another libfheicp.so)."""
+    try:
+        d = json.loads(PMC_FILE.read_text())
+    except (OSError, ValueError):
+        return {}
+    return d.get("kernels", {}) if d.get("lib_sha256") == lib_sha256() else {}
+
+
 def read_br(eng) -> dict:
-    """Blind-rotation HIP-event totals per gadget (fhe_profile_read)."""
-    return {g: eng.profile_read(f"blind_rotate_{g}") for g in ("main", "fast", "fast2")}
+    """Blind-rotation HIP-event totals per gadget (fhe_profile_read) and the
+    instantiation each launched (fhe_profile_kernel_name)."""
+    out = {}
+    for g in ("main", "fast", "fast2"):
+        out[g] = eng.profile_read(f"blind_rotate_{g}")
+        out[g]["kernel"] = eng.kernel_name(f"blind_rotate_{g}")
+    return out
 
 
-def _br_kernel(q, br) -> dict:
-    """One blind-rotation kernel (gadget q) from its own launches."""
+def _br_kernel(q, br, pmc) -> dict:
+    """One blind-rotation kernel (gadget q) from its own launches: HIP-event
+    time per launch; f64 FLOPs executed per launch from the PMC pass of this
+    build at this batch size (else the analytic count); algorithmic HBM bytes
+    (the FFT-domain BSK once + LWE I/O) and the PMC-measured HBM bytes."""
     avg_ms = br["total_ms"] / max(br["launches"], 1)
     cts_per_launch = br["items"] / max(br["launches"], 1)
     bsk_bytes = q.n * (q.k + 1) * q.pbs_level * (q.k + 1) * (q.N // 2) * 16
     io_bytes = cts_per_launch * ((q.n + 1) * 8 + (q.k * q.N + 1) * 8 * 5)
     alg_bytes = bsk_bytes + io_bytes
-    a32 = q.pbs_base_log * q.pbs_level <= 31
+    m = pmc.get(br["kernel"], {})
+    measured = bool(m) and int(m.get("cts_per_launch", -1)) == int(cts_per_launch)
+    flops = float(m["f64_flops_per_launch"]) if measured else br_flops_per_ct(q) * cts_per_launch
+    secs = avg_ms * 1e-3
     return {
-        "kernel": f"k_blind_rotate_v4<{q.pbs_level}, {'true' if a32 else 'false'}, ...> "
-                  f"(gadget ({q.pbs_base_log},{q.pbs_level}))",
+        "kernel": br["kernel"], "gadget": [q.pbs_base_log, q.pbs_level],
         "avg_launch_ms": round(avg_ms, 4), "launches": br["launches"], "cts_per_launch": cts_per_launch,
-        "total_ms": round(br["total_ms"], 3), "alg_bytes_per_launch": int(alg_bytes),
-        "achieved_gbs": alg_bytes / (avg_ms * 1e-3) / 1e9 if br["launches"] else 0.0,
-        "achieved_tflops_f64": br_flops_per_ct(q) * cts_per_launch / (avg_ms * 1e-3) / 1e12 if br["launches"] else 0.0,
+        "total_ms": round(br["total_ms"], 3),
+        "f64_flops_per_launch": flops, "flops_source": "pmc" if measured else "analytic",
+        "achieved_tflops_f64": flops / secs / 1e12 if br["launches"] else 0.0,
+        "alg_bytes_per_launch": int(alg_bytes),
+        "achieved_gbs": alg_bytes / secs / 1e9 if br["launches"] else 0.0,
+        "hbm_bytes_per_launch": float(m["hbm_bytes_per_launch"]) if measured and "hbm_bytes_per_launch" in m else None,
+        "pmc_avg_launch_ms": m.get("avg_launch_ms") if measured else None,
     }
 
 
 def roofline(p, brs) -> dict:
-    """External-product (blind rotation) roofline of the dominant kernel, from
-    the HIP events bracketing each launch on its stream (fhe_profile_read).
-    With fast gadgets the sign rounds run two or three
-    kernels; the one with the larger total time is reported, all are listed."""
+    """Roofline of the dominant blind-rotation (external-product) kernel.
+
+    The kernel is f64-VALU bound (the FFT-domain BSK stream is
+    L2/Infinity-cache resident and its HBM rate is ~0.3% of 8 TB/s), so the
+    roof is the f64 vector peak: achieved = f64 FLOPs executed per launch
+    (rocprofv3 SQ_INSTS_VALU_{FMA,ADD,MUL}_F64 of this exact build, x64 lanes,
+    FMA x2) / the HIP-event launch time on the kernel's stream. The HBM view
+    (algorithmic bytes / time against 8 TB/s, and the PMC-measured bytes as
+    `traffic`) stays beside it. With per-round gadgets two or
+    three kernels run; the one with the largest total time is reported, all
+    are listed under `kernels`."""
     from dataclasses import replace
     qs = {"main": p}
     if p.pbs_fast_level:
         qs["fast"] = replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level)
     if p.pbs_fast2_level:
         qs["fast2"] = replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level)
-    ks = {g: _br_kernel(q, brs[g]) for g, q in qs.items() if brs[g]["launches"]}
+    pmc = load_pmc()
+    ks = {g: _br_kernel(q, brs[g], pmc) for g, q in qs.items() if brs[g]["launches"]}
     dom = max(ks, key=lambda g: ks[g]["total_ms"])
     k = ks[dom]
-    traffic = None
-    tj = REPO / "profiles" / "r01_br_traffic.json"
-    if tj.exists():
-        try:
-            tr = json.loads(tj.read_text())
-            q = qs[dom]
-            if (tr.get("pbs_level"), tr.get("pbs_base_log", q.pbs_base_log)) == (q.pbs_level, q.pbs_base_log) \
-                    and tr.get("kernel_build") == TRAFFIC_BUILD and tr.get("cts_per_launch") == k["cts_per_launch"]:
-                traffic = tr.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    tf = k["achieved_tflops_f64"]
     return {
         "kernel": k["kernel"],
-        "bound": "hbm",
-        "achieved": round(k["achieved_gbs"], 2),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 5),
-        "traffic": traffic,
+        "bound": "f64-valu",
+        "achieved": round(tf, 3),
+        "peak": F64_VALU_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
+        "traffic": k["hbm_bytes_per_launch"],
+        "flops_per_launch": k["f64_flops_per_launch"],
+        "flops_source": k["flops_source"],
         "avg_launch_ms": k["avg_launch_ms"],
         "launches": k["launches"],
         "cts_per_launch": k["cts_per_launch"],
-        "alg_bytes_per_launch": k["alg_bytes_per_launch"],
-        "note": "algorithmic bytes = FFT-domain BSK once per launch + per-ct LWE I/O; the kernel is f64-VALU "
-                "bound, see compute",
-        "compute": {"achieved_tflops_f64": round(k["achieved_tflops_f64"], 2), "peak_tflops_f64": F64_VALU_PEAK_TFLOPS,
-                    "frac": round(k["achieved_tflops_f64"] / F64_VALU_PEAK_TFLOPS, 4)},
+        "hbm": {"alg_bytes_per_launch": k["alg_bytes_per_launch"], "achieved_gbs": round(k["achieved_gbs"], 2),
+                "peak_gbs": HBM_PEAK_GBS, "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 5),
+                "traffic_bytes_per_launch": k["hbm_bytes_per_launch"]},
+        "pmc": {"file": str(PMC_FILE.relative_to(REPO)), "matches_this_build": bool(pmc),
+                "recipe": "f64 FLOPs = 64 x (2 FMA_F64 + ADD_F64 + MUL_F64) wave-instructions; HBM bytes = "
+                          "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 FETCH_SIZE half-count), separate --pmc "
+                          "passes over bench.py --steps 1"},
         "kernels": {g: {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in kv.items()}
                     for g, kv in ks.items()},
     }

@@ -18,9 +18,20 @@ reference's: float ``>=`` threshold, stable descending sort, ``[:top_k]``
 (:282-284).
 
 The upstream text -> vector stage (BertEmbedder + DimensionReducer,
-bert_embeddings.py / dimension_reduction.py) is outside this package: pass
-objects with ``get_embedding(text)`` / ``get_embeddings_batch(texts)`` and
-``transform(X)``; ``search_vector`` takes an already reduced query.
+bert_embeddings.py / dimension_reduction.py) is outside this package. As in
+the reference (:62-64), a processor built without them creates
+``BertEmbedder()`` and ``DimensionReducer.load(config.reducer_path)`` from the
+reference's modules on ``sys.path`` (lazily, on the first text operation, so
+``compare`` never needs BERT), and a processor built without a key manager
+creates ``FHEKeyManager()`` (``BatchConfig.key_manager_default=False`` runs
+standalone instead: no key manager, the model is trained and compiled here).
+``search_vector`` takes an already reduced query.
+
+The reference CLI (fhe_cli.py:32-40) builds ``BatchConfig(show_progress=True)``
+and nothing else, so its knobs come from the environment: ``FHE_ICP_DIM`` and
+``FHE_ICP_N_BITS`` (the model width and quantisation bits, reference: 128 and
+8, batch_operations.py:86) and ``FHE_ICP_FHE`` (execute | simulate | disable;
+the reference's compare/search call predict() in the clear, :233, :276).
 """
 from __future__ import annotations
 
@@ -28,7 +39,7 @@ import gc
 import hashlib
 import logging
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from datetime import datetime
 from typing import Dict, List, Optional, Tuple
 
@@ -51,9 +62,13 @@ class BatchConfig:
     show_progress: bool = True
     force_gc: bool = True
     # engine fields
-    fhe: str = "execute"            # how compare/search evaluate the model
-    input_dim: int = 128            # the reference hard-codes 128 (:86)
-    n_bits: int = 8                 # and 8 (:86)
+    fhe: str = field(default_factory=lambda: os.environ.get("FHE_ICP_FHE", "execute"))
+    # the reference hard-codes 128 and 8 (:86); --dim / --n-bits knobs of an
+    # unchanged fhe_cli via FHE_ICP_DIM / FHE_ICP_N_BITS
+    input_dim: int = field(default_factory=lambda: int(os.environ.get("FHE_ICP_DIM", "128")))
+    n_bits: int = field(default_factory=lambda: int(os.environ.get("FHE_ICP_N_BITS", "8")))
+    reducer_path: str = "pca_reducer_128.pkl"  # DimensionReducer.load (:63)
+    key_manager_default: bool = True  # no key_manager given: FHEKeyManager() as the reference (:64)
     device: int = 0
     model_path: Optional[str] = None  # fheicp.persist file: load instead of retrain (§8f-2)
     seed: Optional[int] = None      # training-data seed when no model_path
@@ -76,6 +91,8 @@ class BatchConfig:
             raise ValueError(f"fhe must be one of {FHE_MODES}")
         if self.search_chunk < 1:
             raise ValueError("search_chunk must be >= 1")
+        if self.input_dim < 1 or not 2 <= self.n_bits <= 16:
+            raise ValueError("input_dim must be >= 1 and n_bits in [2, 16]")
 
 
 class BatchProcessor:
@@ -84,9 +101,12 @@ class BatchProcessor:
                  fhe_model: Optional[FHESimilarityModel] = None):
         self.embedder = embedder
         self.reducer = reducer
+        self.config = config if config is not None else BatchConfig()
+        if key_manager is None and self.config.key_manager_default:
+            from key_management import FHEKeyManager
+            key_manager = FHEKeyManager()
         self.key_manager = key_manager
         self.storage = storage if storage is not None else EncryptedDocumentStore()
-        self.config = config if config is not None else BatchConfig()
         if self.config.input_dim not in (EncryptedDocument.allowed_dims or (self.config.input_dim,)):
             EncryptedDocument.allowed_dims = tuple(sorted(set(DEFAULT_DIMS) | {self.config.input_dim}))
         self._resident = None  # (host array identity, device tensor)
@@ -208,11 +228,22 @@ class BatchProcessor:
         }
 
     # --------------------------------------------------------- documents --
+    def _upstream(self):
+        """The embedder and reducer, created as the reference does on first
+        use (:62-63): ``bert_embeddings.BertEmbedder()`` and
+        ``dimension_reduction.DimensionReducer.load(config.reducer_path)``
+        from the reference's modules on sys.path."""
+        if self.embedder is None:
+            from bert_embeddings import BertEmbedder
+            self.embedder = BertEmbedder()
+        if self.reducer is None:
+            from dimension_reduction import DimensionReducer
+            self.reducer = DimensionReducer.load(self.config.reducer_path)
+        return self.embedder, self.reducer
+
     def _embed(self, texts: List[str]) -> np.ndarray:
-        if self.embedder is None or self.reducer is None:
-            raise RuntimeError("encrypt_documents/search_similar need an embedder and a reducer "
-                               "(BERT + PCA are upstream of this package)")
-        return self.reducer.transform(self.embedder.get_embeddings_batch(texts))
+        embedder, reducer = self._upstream()
+        return reducer.transform(embedder.get_embeddings_batch(texts))
 
     def encrypt_documents(self, texts: List[str], doc_ids: Optional[List[str]] = None,
                           metadata: Optional[List[Dict]] = None) -> List[str]:
@@ -300,10 +331,9 @@ class BatchProcessor:
     # ------------------------------------------------------------ search --
     def search_similar(self, query_text: str, top_k: int = 5, min_similarity: float = 0.5) -> List[Tuple[str, float]]:
         self._require_model()
-        if self.embedder is None or self.reducer is None:
-            raise RuntimeError("search_similar needs an embedder and a reducer; use search_vector")
-        q = self.embedder.get_embedding(query_text)
-        q = self.reducer.transform(np.asarray(q).reshape(1, -1))[0]
+        embedder, reducer = self._upstream()
+        q = embedder.get_embedding(query_text)
+        q = reducer.transform(np.asarray(q).reshape(1, -1))[0]
         return self.search_vector(q, top_k, min_similarity)
 
     def search_vector(self, query: np.ndarray, top_k: int = 5, min_similarity: float = 0.5) -> List[Tuple[str, float]]:

@@ -32,6 +32,7 @@ struct ProfAcc {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   double ms = 0;
   int64_t launches = 0, items = 0;
+  const char* kernel = nullptr;  // the last launched instantiation (rocprofv3's name)
 };
 
 struct fhe_ctx {
@@ -50,10 +51,12 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
   bool prof = false;
   ProfAcc prof_br, prof_brf[2], prof_ks;  // blind rotation on the main / fast / fast2 gadget
+  int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2
+                       // (two waves per ciphertext; forced by FHEICP_BR_VARIANT=2), 3 (A/B builds)
+  // A/B builds only (FHEICP_AB, tools/build_variant.sh): other v4 shapes
   int v4_g = 4;        // v4 ciphertexts per workgroup (FHEICP_V4_G = 1, 2 or 4)
   int v4_fl = 0;       // v4 per-ciphertext LDS hand-offs instead of s_barrier (FHEICP_V4_FL=1)
-  int v4_a64 = 0;      // v4: 64-bit accumulators even where 32 bits suffice (FHEICP_V4_A64=1, A/B)
-  int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2, 3
+  int v4_a64 = 0;      // v4: 64-bit accumulators even where 32 bits suffice (FHEICP_V4_A64=1)
   int v4_dbg = 0;      // timing experiments only (FHEICP_V4_DBG), wrong results
   // i8-MFMA key switch: key byte planes and a digit/body workspace
   int8_t* ksk8 = nullptr;
@@ -119,11 +122,19 @@ static double tuniform_var(int b) { return (std::ldexp(1.0, 2 * b + 1) + 1.0) / 
 
 // Noise model, the same formulas as fheicp/params.py and
 // oracle/tfhe_ref.c; variances relative to the 2^64 torus.
+// Bootstrap output variance: key noise + gadget rounding + the f64 FFT's
+// arithmetic error (C_FFT = 16 bounds the 11.6-13.8 measured on every kernel
+// instance, tests/test_gpu_noise.py) + the 2^32 rounding of the 32-bit
+// accumulators (L*beta <= 31), the last two key-weighted per step.
+constexpr double C_FFT = 16.0;
 static double pbs_var(const fhe_params& p, int beta, int L) {
   const double s2_bsk = tuniform_var(p.glwe_noise_bits) / std::ldexp(1.0, 128);
   const double B = std::ldexp(1.0, beta);
   const double rows = (double)L * (p.k + 1) * p.N;
-  return p.n * rows * (B * B + 2) / 12.0 * s2_bsk + p.n * (1 + p.k * p.N / 2.0) / (12.0 * std::pow(B, 2.0 * L));
+  const double steps = p.n * (1 + p.k * p.N / 2.0);
+  double arith = C_FFT * rows * B * B / 144.0 * std::ldexp(1.0, -106);
+  if (beta * L <= 31) arith += std::ldexp(1.0, -64) / 12.0;
+  return p.n * rows * (B * B + 2) / 12.0 * s2_bsk + steps / (12.0 * std::pow(B, 2.0 * L)) + steps * arith;
 }
 static double ks_var(const fhe_params& p) {
   const double s2_ksk = tuniform_var(p.lwe_noise_bits) / std::ldexp(1.0, 128);
@@ -246,8 +257,12 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   ctx->device = device;
   if (const char* e = getenv("FHEICP_BR_VARIANT")) {
     const int v = atoi(e);
-    ctx->br_variant = (v == 2 || v == 3 || v == 4) ? v : 4;
+    ctx->br_variant = (v == 2 || v == 4) ? v : 4;
+#ifdef FHEICP_AB
+    if (v == 3) ctx->br_variant = 3;
+#endif
   }
+#ifdef FHEICP_AB
   if (const char* e = getenv("FHEICP_V4_DBG")) ctx->v4_dbg = atoi(e);
   if (const char* e = getenv("FHEICP_V4_G")) {
     const int g = atoi(e);
@@ -255,6 +270,7 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   }
   if (const char* e = getenv("FHEICP_V4_FL")) ctx->v4_fl = atoi(e) != 0;
   if (const char* e = getenv("FHEICP_V4_A64")) ctx->v4_a64 = atoi(e) != 0;
+#endif
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
   if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
@@ -422,8 +438,10 @@ static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* b
       if (variant_for(ctx, p) == 4)
         hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, bsk, npoly, ctx->tw4,
                            bsk_fft, (v4_a32(ctx, p) ? 1.0 / 18446744073709551616.0 : 1.0) / (double)(p.N / 2));
+#ifdef FHEICP_AB
       else if (variant_for(ctx, p) == 3)
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
+#endif
       else
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
       break;
@@ -544,6 +562,21 @@ int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_
   ChaKey K = key_from_seed(seed);
   hipLaunchKernelGGL(k_encrypt, dim3((unsigned)count), dim3(256), 0, (hipStream_t)stream, K, p.k * p.N, p.msg_bits,
                      p.glwe_noise_bits, ctx->s_big, d_msg, id0, d_ct);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
+                             const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_out))) return fail(ctx, FHE_E_ARG, "bad encrypt-linear arguments");
+  if (B == 0) return FHE_OK;
+  if (B > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "encrypt-linear batch too large: split the call");
+  const fhe_params& p = ctx->p;
+  const ChaKey K = key_from_seed(seed);
+  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, K, p.k * p.N, p.msg_bits,
+                     p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, d_w, ((u64)cst) << (64 - p.msg_bits), id0, d_out);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -688,6 +721,7 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
     u64* body = (u64*)((char*)ctx->ks_ws + dbytes);
     hipEvent_t e1;
     prof_begin(ctx, ctx->prof_ks, st, &e1);
+    ctx->prof_ks.kernel = "k_keyswitch_mfma";
     hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)KB, (unsigned)ncb), dim3(256), 0, st, d_big, count, p.k * p.N,
                        p.ks_base_log, shift, add_body, KB, D, body);
     hipLaunchKernelGGL(k_keyswitch_mfma, dim3((unsigned)((count + 63) / 64), (unsigned)NB), dim3(256), 0, st,
@@ -699,6 +733,7 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   HIPCHK(ctx, hipMemsetAsync(d_small, 0, 8 * (size_t)count * (p.n + 1), st));
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_ks, st, &e1);
+  ctx->prof_ks.kernel = "k_keyswitch";
   hipLaunchKernelGGL(k_keyswitch, dim3((p.n + 1 + 255) / 256, (unsigned)tiles, KS_SPLIT), dim3(256), 0, st, d_big,
                      count, p.k * p.N, p.n, p.ks_level, p.ks_base_log, shift, add_body, ctx->ksk, ctx->ksk_colsum,
                      d_small);
@@ -707,8 +742,48 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   return FHE_OK;
 }
 
+#ifdef FHEICP_AB
+// A/B-only v4 shapes (FHEICP_V4_G = 1 or 2 for the 32-bit-accumulator
+// kernels, FHEICP_V4_FL per-ciphertext hand-offs, FHEICP_V4_DBG timing
+// experiments); false when the shipped dispatch applies.
+static bool launch_br_ab(fhe_ctx* ctx, const fhe_params& p, const uint64_t* d_small, int64_t count, const BrTv& tv, int mode, uint64_t* out,
+                         uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, const c64* bsk_fft, hipStream_t st,
+                         const char** name) {
+  const bool a32 = v4_a32(ctx, p);
+#define AB4(L, A32, D, GG, FLAGS)                                                                               do {                                                                                                            hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),                           dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft,                               ctx->tw4, tv, mode, out, ct_v, refreshed, sign);                                           *name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ">";                                    return true;                                                                                                } while (0)
+#define AB4G(L, A32, D, GG)   do { if (ctx->v4_fl && GG > 1) AB4(L, A32, D, GG, true); else AB4(L, A32, D, GG, false); } while (0)
+#define AB4D(D)   do { if (ctx->v4_g == 1) AB4G(2, true, D, 1); else if (ctx->v4_g == 2) AB4G(2, true, D, 2); else AB4G(2, true, D, 4); } while (0)
+  if (ctx->v4_dbg && p.pbs_level == 2 && a32) {
+    switch (ctx->v4_dbg) {
+      case 1: AB4D(1); case 2: AB4D(2); case 4: AB4D(4); case 8: AB4D(8); case 16: AB4D(16);
+      case 32: AB4D(32); case 6: AB4D(6); case 128: AB4D(128); default: AB4D(63);
+    }
+  }
+  if (!(ctx->v4_g == 1 || ctx->v4_fl || (a32 && ctx->v4_g == 2) || (!a32 && ctx->v4_g == 4))) return false;
+  const int G = ctx->v4_g;
+  switch (p.pbs_level) {
+    case 1:
+      if (a32) { if (G == 1) AB4G(1, true, 0, 1); else if (G == 2) AB4G(1, true, 0, 2); else AB4G(1, true, 0, 4); }
+      else { if (G == 1) AB4G(1, false, 0, 1); else if (G == 2) AB4G(1, false, 0, 2); else AB4G(1, false, 0, 4); }
+      break;
+    case 2:
+      if (a32) { if (G == 1) AB4G(2, true, 0, 1); else if (G == 2) AB4G(2, true, 0, 2); else AB4G(2, true, 0, 4); }
+      else { if (G == 1) AB4G(2, false, 0, 1); else if (G == 2) AB4G(2, false, 0, 2); else AB4G(2, false, 0, 4); }
+      break;
+    case 3:
+      if (G == 1) AB4G(3, false, 0, 1); else if (G == 2) AB4G(3, false, 0, 2); else AB4G(3, false, 0, 4);
+      break;
+  }
+#undef AB4
+#undef AB4G
+#undef AB4D
+  return false;
+}
+#endif
+
 // gad = 1 / 2: the fast / fast2 gadget and its key (fhe_params.pbs_fast*_*),
-// else the main one
+// else the main one. The launched instantiation's name (as rocprofv3 prints
+// it) is recorded in the profile bucket (fhe_profile_kernel_name).
 static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv tv, int mode, uint64_t* out,
                      uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, hipStream_t st, int gad = 0) {
   const bool fast = gad > 0 && fast_level(ctx->p, gad);
@@ -718,71 +793,61 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   hipEvent_t e1;
   ProfAcc& prof = fast ? ctx->prof_brf[gad - 1] : ctx->prof_br;
   prof_begin(ctx, prof, st, &e1);
+  const char* name = nullptr;
   const dim3 g((unsigned)count), b(64);
 #define BR(LOGM, K)                                                                                           \
-  hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,      \
-                     bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
+  do {                                                                                                        \
+    hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,    \
+                       bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign);                  \
+    name = "k_blind_rotate<" #LOGM ", " #K ">";                                                               \
+  } while (0)
 #define BRV(V, K, W)                                                                                          \
-  hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,          \
-                     p.pbs_base_log, bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign)
-#define BR2(K) do { if (var == 3) BRV(V3, K, 4); else BRV(V2, K, 2); } while (0)
-#define BR4G(L, A32, D, GG)                                                                                   \
-  if (ctx->v4_fl && GG > 1) BR4F(L, A32, D, GG, true); else BR4F(L, A32, D, GG, false)
-#define BR4F(L, A32, D, GG, FLAGS)                                                                             \
-  hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),       \
-                     dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, tv, \
-                     mode, out, ct_v, refreshed, sign)
-// G = 4 needs 3 waves per SIMD (<= 168 VGPRs): only the 32-bit-accumulator
-// kernels; the u64 ones (208 VGPRs, 2 waves per SIMD) run 2 per workgroup
-// (at 4 per workgroup they spill: P=21, 22.2 vs 20.9 ms per 1024 PBS).
-#define BR4(L, A32)                                  \
-  do {                                               \
-    if (ctx->v4_g == 1) BR4G(L, A32, 0, 1);          \
-    else if (ctx->v4_g == 2 || !A32) BR4G(L, A32, 0, 2); \
-    else BR4G(L, A32, 0, 4);                         \
+  do {                                                                                                        \
+    hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,        \
+                       p.pbs_base_log, bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign);   \
+    name = "k_blind_rotate_mw<fhei::" #V ", " #K ", " #W ">";                                                 \
   } while (0)
-#define BR4D(D)                                      \
-  do {                                               \
-    if (ctx->v4_g == 1) BR4G(2, true, D, 1);         \
-    else if (ctx->v4_g == 2) BR4G(2, true, D, 2);    \
-    else BR4G(2, true, D, 4);                        \
+#define BR4F(L, A32, D, GG, FLAGS)                                                                            \
+  do {                                                                                                        \
+    hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),    \
+                       dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, \
+                       tv, mode, out, ct_v, refreshed, sign);                                                 \
+    name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ">";                                 \
   } while (0)
-  if (p.N == 1024 && p.k == 2 && var == 4 && ctx->v4_dbg && p.pbs_level == 2 &&
-      v4_a32(ctx, p)) {
-    switch (ctx->v4_dbg) {
-      case 1: BR4D(1); break;
-      case 2: BR4D(2); break;
-      case 4: BR4D(4); break;
-      case 8: BR4D(8); break;
-      case 16: BR4D(16); break;
-      case 32: BR4D(32); break;
-      case 6: BR4D(6); break;
-      case 128: BR4D(128); break;
-      default: BR4D(63); break;
-    }
+  // The shipped v4 instances: 4 ciphertexts per workgroup (3 waves per SIMD,
+  // <= 168 VGPRs) for the 32-bit-accumulator kernels; 2 for the u64 ones
+  // (208+ VGPRs; at 4 per workgroup they spill: P=21, 22.2 vs 20.9 ms per
+  // 1024 bootstraps). Other shapes are A/B builds (FHEICP_AB).
+  bool done = false;
+#ifdef FHEICP_AB
+  if (p.N == 1024 && p.k == 2 && var == 4) done = launch_br_ab(ctx, p, d_small, count, tv, mode, out, ct_v, refreshed, sign,
+                                                               bsk_fft, st, &name);
+  if (p.N == 1024 && var == 3) {
+    if (p.k == 1) BRV(V3, 1, 4); else BRV(V3, 2, 4);
+    done = true;
+  }
+#endif
+  if (done) {
   } else if (p.N == 1024 && p.k == 2 && var == 4) {
     const bool a32 = v4_a32(ctx, p);
     switch (p.pbs_level) {
-      case 1: if (a32) BR4(1, true); else BR4(1, false); break;
-      case 2: if (a32) BR4(2, true); else BR4(2, false); break;
-      case 3: BR4(3, false); break;
+      case 1: if (a32) BR4F(1, true, 0, 4, false); else BR4F(1, false, 0, 2, false); break;
+      case 2: if (a32) BR4F(2, true, 0, 4, false); else BR4F(2, false, 0, 2, false); break;
+      case 3: BR4F(3, false, 0, 2, false); break;
       default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: pbs_level > 3");
     }
   } else if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
   else if (p.N == 512 && p.k == 1) BR(8, 1);
   else if (p.N == 512 && p.k == 2) BR(8, 2);
-  else if (p.N == 1024 && p.k == 1) BR2(1);
-  else if (p.N == 1024 && p.k == 2) BR2(2);
+  else if (p.N == 1024 && p.k == 1) BRV(V2, 1, 2);
+  else if (p.N == 1024 && p.k == 2) BRV(V2, 2, 2);
   else if (p.N == 2048 && p.k == 1) BR(10, 1);
   else return fail(ctx, FHE_E_ARG, "unsupported (N, k)");
 #undef BR
-#undef BR2
-#undef BR4
-#undef BR4D
-#undef BR4G
 #undef BR4F
 #undef BRV
+  prof.kernel = name;
   prof_end(ctx, prof, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
@@ -812,6 +877,22 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
   if (count == 0) return FHE_OK;
   return launch_br(ctx, d_small, count, BrTv{base, step, logN - log_slots}, 0, d_out, nullptr, nullptr, nullptr,
                    (hipStream_t)stream);
+}
+
+int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const int64_t* d_lut, int32_t lut_bits,
+                        uint64_t* d_out, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  const int logN = log2i(ctx->p.N);
+  if (count < 0 || lut_bits < 0 || lut_bits > logN - 1 || !d_lut || (count > 0 && (!d_small || !d_out)))
+    return fail(ctx, FHE_E_ARG, "bad pbs-table arguments (0 <= lut_bits <= log2(N) - 1)");
+  if (count == 0) return FHE_OK;
+  BrTv tv{0, 0, 0};
+  tv.lut = d_lut;
+  tv.lut_count = 1 << lut_bits;
+  tv.lut_log_box = logN - lut_bits;
+  tv.delta = 1ull << (64 - ctx->p.msg_bits);
+  return launch_br(ctx, d_small, count, tv, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
 }
 
 static int ensure_ws(fhe_ctx* ctx, size_t bytes) {
@@ -964,22 +1045,17 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   const fhe_params& p = ctx->p;
   hipStream_t st = (hipStream_t)stream;
   const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
-  // workspace: inputs (B*D big) | ct_v (B big) | sign (B big) | small (B) | v (B)
-  const size_t bytes = 8 * ((size_t)B * D * Wb + 2 * (size_t)B * Wb + (size_t)B * Ws + (size_t)B);
+  // workspace: ct_v (B big) | sign (B big) | small (B) | v (B); the B x D
+  // input ciphertexts are never materialised (k_encrypt_linear)
+  const size_t bytes = 8 * (2 * (size_t)B * Wb + (size_t)B * Ws + (size_t)B);
   rc = ensure_ws(ctx, bytes);
   if (rc) return rc;
-  u64* cin = (u64*)ctx->ws;
-  u64* ctv = cin + (size_t)B * D * Wb;
+  u64* ctv = (u64*)ctx->ws;
   u64* sgn = ctv + (size_t)B * Wb;
   u64* small = sgn + (size_t)B * Wb;
   int64_t* v = (int64_t*)(small + (size_t)B * Ws);
-  rc = fhe_encrypt_batch(ctx, d_qx, B * D, enc_seed, id0, cin, stream);
+  rc = fhe_encrypt_linear_batch(ctx, d_qx, B, D, enc_seed, id0, d_w, cst - T, ctv, stream);
   if (rc) return rc;
-  for (int64_t b0 = 0; b0 < B; b0 += 65535) {
-    const int64_t nb = std::min<int64_t>(65535, B - b0);
-    rc = fhe_linear_batch(ctx, cin + (size_t)b0 * D * Wb, nb, D, d_w, cst - T, ctv + (size_t)b0 * Wb, stream);
-    if (rc) return rc;
-  }
   // The score comes from the leveled accumulator ciphertext (noise ~2^20,
   // as in the reference's leveled Concrete circuit); the PBS chain then
   // computes the encrypted threshold bit [acc < T] exactly.
@@ -1021,6 +1097,33 @@ int fhe_compare_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_
   rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_threshold_batch(fhe_ctx* ctx, const uint64_t* d_ct_acc, int64_t count, int64_t T, uint64_t* d_bit,
+                        void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || (count > 0 && (!d_ct_acc || !d_bit))) return fail(ctx, FHE_E_ARG, "bad threshold arguments");
+  if (count == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
+  // workspace: v = acc - T (B big, consumed by the extraction) | small (B)
+  rc = ensure_ws(ctx, 8 * ((size_t)count * Wb + (size_t)count * Ws));
+  if (rc) return rc;
+  u64* ctv = (u64*)ctx->ws;
+  u64* small = ctv + (size_t)count * Wb;
+  const int64_t words = count * (int64_t)Wb;
+  hipLaunchKernelGGL(k_lwe_affine, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, d_ct_acc, count, (int)Wb,
+                     (u64)1, (u64)0 - ((u64)T << (64 - p.msg_bits)), ctv);
+  HIPCHK(ctx, hipGetLastError());
+  rc = sign_extract(ctx, ctv, count, d_bit, small, st);
+  if (rc) return rc;
+  // [acc >= T] = 1 - [v < 0]: negate the sign ciphertext and add 2^63 to its body
+  hipLaunchKernelGGL(k_lwe_affine, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, d_bit, count, (int)Wb,
+                     (u64)0 - 1, 1ull << 63, d_bit);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -1127,9 +1230,38 @@ int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out) {
   int rc = need_device(ctx);
   if (rc) return rc;
   if (!h_out) return fail(ctx, FHE_E_ARG, "null output");
+#ifndef FHEICP_AB
+  return fail(ctx, FHE_E_STATE, "phase stamps need an A/B build (FHEICP_AB, tools/build_variant.sh)");
+#endif
   HIPCHK(ctx, hipDeviceSynchronize());
   HIPCHK(ctx, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_v4_stamps), sizeof(unsigned long long) * 64));
   HIPCHK(ctx, hipMemcpyFromSymbol(h_out + 64, HIP_SYMBOL(g_v4_span), sizeof(unsigned long long) * 2048 * 3));
+  return FHE_OK;
+}
+
+const char* fhe_build_info(void) {
+#ifdef FHEICP_AB
+  return "libfheicp gfx950 ab=1";
+#else
+  return "libfheicp gfx950 ab=0";
+#endif
+}
+
+static ProfAcc* prof_bucket(fhe_ctx* ctx, const char* kernel) {
+  if (!strcmp(kernel, "blind_rotate") || !strcmp(kernel, "blind_rotate_main")) return &ctx->prof_br;
+  if (!strcmp(kernel, "blind_rotate_fast")) return &ctx->prof_brf[0];
+  if (!strcmp(kernel, "blind_rotate_fast2")) return &ctx->prof_brf[1];
+  if (!strcmp(kernel, "keyswitch")) return &ctx->prof_ks;
+  return nullptr;
+}
+
+int fhe_profile_kernel_name(fhe_ctx* ctx, const char* kernel, char* h_buf, size_t len) {
+  if (!ctx) return fail(nullptr, FHE_E_ARG, "null ctx");
+  if (!kernel || !h_buf || len == 0) return fail(ctx, FHE_E_ARG, "null kernel name or buffer");
+  ProfAcc* a = prof_bucket(ctx, kernel);
+  if (!a) return fail(ctx, FHE_E_ARG, "unknown kernel name");
+  const char* nm = a->kernel ? a->kernel : "";
+  snprintf(h_buf, len, "%s", nm);
   return FHE_OK;
 }
 

@@ -1,10 +1,13 @@
-// Blind rotation kernels: v1 (one wave), v2/v3 (br_m512*.h), v4 (br_v4.h, the default).
+// Blind rotation kernels: v1 (one wave), v2 (br_m512.h), v4 (br_v4.h, the default);
+// v3 (br_m512q.h) only in A/B builds (FHEICP_AB, tools/build_variant.sh).
 // Part of libfheicp (one translation unit: fheicp.hip includes it).
 #pragma once
 
 #include "common.h"
 #include "br_m512.h"
+#ifdef FHEICP_AB
 #include "br_m512q.h"
+#endif
 #include "br_v4.h"
 
 template <int LOGM, int K>

@@ -145,6 +145,50 @@ __global__ void __launch_bounds__(256) k_encrypt(ChaKey K, int dim, int msg_bits
 // a PUBLIC mask key Km, the noise stream(TAG_ENC_NOISE, id) of a SECRET
 // noise key Kn. Document b of a corpus holds D bodies,
 // feature j under stream id id0[b] + j. 2049 -> 1 word per feature in HBM:
+// Fused fresh encryption + leveled dot product (fhe_encrypt_linear_batch):
+// out[b] = sum_j w[j] * Enc(x[b, j]) + trivial(cst) without materialising the
+// B x D input ciphertexts. Feature j of pair b is encrypted exactly as
+// k_encrypt would (mask stream (TAG_ENC_MASK, id0 + b*D + j), noise word 0 of
+// (TAG_ENC_NOISE, same id)); arithmetic mod 2^64 is linear, so the output is
+// bit-identical to k_encrypt followed by k_linear:
+//   mask = sum_j w_j a_j,  body = <mask, s> + sum_j w_j (e_j + x_j Delta) + cst.
+// One 256-thread workgroup per pair; thread t owns mask words [8t', 8t'+8)
+// for t' = t, t + 256, ...
+__global__ void __launch_bounds__(256) k_encrypt_linear(ChaKey K, int dim, int msg_bits, int noise_bits,
+                                                        const u64* __restrict__ s_big, const int64_t* __restrict__ x,
+                                                        int D, const int64_t* __restrict__ w, u64 cst_scaled,
+                                                        u64 id0, u64* __restrict__ out) {
+  __shared__ u64 red[4];
+  const int64_t b = blockIdx.x;
+  const u64 base = id0 + (u64)b * (u64)D;
+  u64* o = out + (size_t)b * (dim + 1);
+  u64 part = 0;
+  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
+    u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < D; ++j) {
+      u64 m[8];
+      stream_block(K, TAG_ENC_MASK, base + (u64)j, (uint32_t)blk, m);
+      const u64 wj = (u64)w[j];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * m[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[8 * blk + q] = acc[q];
+      part += acc[q] & (0 - s_big[8 * blk + q]);
+    }
+  }
+  const u64 sdot = block_sum_u64<256>(part, red);
+  // the body's per-feature terms, split over the workgroup
+  u64 bpart = 0;
+  for (int j = threadIdx.x; j < D; j += 256) {
+    const u64 e = (u64)tuniform(stream_word(K, TAG_ENC_NOISE, base + (u64)j, 0), noise_bits);
+    bpart += (u64)w[j] * (e + ((u64)x[(size_t)b * D + j] << (64 - msg_bits)));
+  }
+  const u64 bsum = block_sum_u64<256>(bpart, red);
+  if (threadIdx.x == 0) o[dim] = sdot + bsum + cst_scaled;
+}
+
 // the masks are regenerated where they are consumed (k_linear_seeded).
 __global__ void __launch_bounds__(256) k_encrypt_seeded(ChaKey Km, ChaKey Kn, int dim, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big,

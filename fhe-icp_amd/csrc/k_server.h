@@ -239,6 +239,15 @@ __global__ void k_add_scalar(const int64_t* __restrict__ v, int64_t B, int64_t T
   if (i < B) out[i] = v[i] + T;
 }
 
+// out = mul * ct + trivial(add) for count LWEs of W words (in place allowed):
+// every word times mul mod 2^64, `add` on the body
+__global__ void k_lwe_affine(const u64* in, int64_t count, int W, u64 mul, u64 add, u64* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count * W) return;
+  const u64 x = in[i] * mul;
+  out[i] = (i % W == W - 1) ? x + add : x;
+}
+
 // Single-workgroup top-k by (acc desc, idx asc) over entries not below the
 // threshold. k passes; pass p selects the largest key strictly smaller than
 // the key chosen in pass p-1 (keys are unique because indices are).

@@ -9,7 +9,11 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libfheicp.so"
+import os
+
+# FHEICP_LIB selects another build (A/B runs: tools/build_variant.sh); the
+# default is the in-tree product library
+LIB_PATH = Path(os.environ.get("FHEICP_LIB") or Path(__file__).resolve().parent / "libfheicp.so").resolve()
 
 FHE_OK = 0
 ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOMEM"}
@@ -53,6 +57,7 @@ SIGNATURES = [
     ("fhe_decrypt_bits_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_phase_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+    ("fhe_encrypt_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _u64, _vp, _i64, _vp, _vp]),
     ("fhe_keyswitch_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
     ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
     ("fhe_bit_extract_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp, _vp]),
@@ -62,6 +67,8 @@ SIGNATURES = [
     ("fhe_sign_precise_rounds", C.c_int, [_P]),
     ("fhe_sign_plan", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
+    ("fhe_pbs_table_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _i32, _vp, _vp]),
+    ("fhe_threshold_batch", C.c_int, [_CTXP, _vp, _i64, _i64, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     ("fhe_encrypt_seeded_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("fhe_expand_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
@@ -79,6 +86,8 @@ SIGNATURES = [
     ("fhe_debug_v4_stamps", C.c_int, [_CTXP, _vp]),
     ("fhe_profile_enable", C.c_int, [_CTXP, C.c_int]),
     ("fhe_profile_read", C.c_int, [_CTXP, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64), C.POINTER(_i64)]),
+    ("fhe_profile_kernel_name", C.c_int, [_CTXP, C.c_char_p, C.c_char_p, C.c_size_t]),
+    ("fhe_build_info", C.c_char_p, []),
 ]
 
 _lib = None
@@ -104,6 +113,11 @@ def lib() -> C.CDLL:
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def ab_build() -> bool:
+    """True for an A/B build (fhe_build_info: extra kernel shapes, timing kernels)."""
+    return b"ab=1" in (lib().fhe_build_info() or b"")
 
 
 def check(rc: int, ctx=None) -> None:

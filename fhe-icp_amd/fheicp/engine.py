@@ -152,6 +152,16 @@ class Engine:
                                            _stream(self.device)))
         return out
 
+    def encrypt_linear(self, msg, w, cst: int, seed: int, id0: int = 0) -> torch.Tensor:
+        """Fused encrypt + linear (fhe_encrypt_linear_batch): msg B x D ints."""
+        m = self.to_dev(msg)
+        B, D = m.shape
+        wd = self.to_dev(w)
+        out = self.empty_big(B)
+        self._chk(self._L.fhe_encrypt_linear_batch(self._ctx, _ptr(m), B, D, C.c_uint64(seed), C.c_uint64(id0),
+                                                   _ptr(wd), int(cst), _ptr(out), _stream(self.device)))
+        return out
+
     def keyswitch(self, ct: torch.Tensor, shift: int = 0, add_body: int = 0) -> torch.Tensor:
         n = ct.numel() // self.W
         out = self.empty_small(n)
@@ -172,6 +182,23 @@ class Engine:
         self._chk(self._L.fhe_pbs_lut_batch(self._ctx, _ptr(small), n, C.c_uint64(base), C.c_uint64(step),
                                             int(log_slots), _ptr(out), _stream(self.device)))
         return out
+
+    def pbs_table(self, small: torch.Tensor, lut, lut_bits: int) -> torch.Tensor:
+        """Table bootstrap (fhe_pbs_table_batch): input m in [0, 2^lut_bits) at
+        2^(63 - lut_bits); output lut[m] at 2^(64 - msg_bits)."""
+        n = small.numel() // self.Ws
+        lut_d = self.to_dev(np.asarray(lut, dtype=np.int64)) if not isinstance(lut, torch.Tensor) else lut
+        out = self.empty_big(n)
+        self._chk(self._L.fhe_pbs_table_batch(self._ctx, _ptr(small), n, _ptr(lut_d), int(lut_bits), _ptr(out),
+                                              _stream(self.device)))
+        return out
+
+    def threshold(self, ct_acc: torch.Tensor, T: int) -> torch.Tensor:
+        """Encryption of [acc >= T] at 2^63 (fhe_threshold_batch); ct_acc is kept."""
+        n = ct_acc.numel() // self.W
+        bit = self.empty_big(n)
+        self._chk(self._L.fhe_threshold_batch(self._ctx, _ptr(ct_acc), n, int(T), _ptr(bit), _stream(self.device)))
+        return bit
 
     def sign(self, ct_v: torch.Tensor) -> torch.Tensor:
         """Consumes ct_v; returns the encryption of [v < 0] at 2^63 (fhe_sign_batch)."""
@@ -263,6 +290,12 @@ class Engine:
     # --------------------------------------------------------- measurement --
     def profile(self, enable: bool) -> None:
         self._chk(self._L.fhe_profile_enable(self._ctx, int(enable)))
+
+    def kernel_name(self, kernel: str) -> str:
+        """The instantiation last launched for a profile bucket (fhe_profile_kernel_name)."""
+        buf = C.create_string_buffer(256)
+        self._chk(self._L.fhe_profile_kernel_name(self._ctx, kernel.encode(), buf, 256))
+        return buf.value.decode()
 
     def profile_read(self, kernel: str) -> dict:
         ms = C.c_double()

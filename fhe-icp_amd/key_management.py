@@ -115,48 +115,62 @@ class FHEKeyManager:
         return self._master_key
 
     # -------------------------------------------------------------- keys --
-    def generate_keys(self, key_id: Optional[str] = None, input_dim: int = 128, n_bits: int = 8,
-                      device: int = 0, seed: Optional[int] = None, key_seed: Optional[int] = None) -> Dict[str, str]:
+    def generate_keys(self, key_id: Optional[str] = None, input_dim: Optional[int] = None,
+                      n_bits: Optional[int] = None, device: int = 0, seed: Optional[int] = None,
+                      key_seed: Optional[int] = None, fhe: Optional[str] = None) -> Dict[str, str]:
         """Train + compile the similarity model (GPU keygen) and store it
-        (key_management.py:112-191; the reference fixes input_dim=128, n_bits=8)."""
+        (key_management.py:112-191; the reference fixes input_dim=128, n_bits=8;
+        here $FHE_ICP_DIM / $FHE_ICP_N_BITS when not given, as for
+        BatchConfig). With fhe != "execute" ($FHE_ICP_FHE; the reference's
+        compare/search predict in the clear) only the quantized model is
+        stored: no keys are generated and no GPU is needed."""
         from fhe_similarity import FHESimilarityModel
         if key_id is None:
             key_id = f"fhe_key_{datetime.now().strftime('%Y%m%d_%H%M%S')}"
+        input_dim = int(input_dim if input_dim is not None else os.environ.get("FHE_ICP_DIM", "128"))
+        n_bits = int(n_bits if n_bits is not None else os.environ.get("FHE_ICP_N_BITS", "8"))
+        fhe = fhe if fhe is not None else os.environ.get("FHE_ICP_FHE", "execute")
         logger.info("Generating new FHE keys with ID: %s", key_id)
         model = FHESimilarityModel(input_dim=input_dim, n_bits=n_bits, device=device, seed=seed)
         X_train, _ = model.train()
+        info = {"input_dim": model.input_dim, "n_bits": model.n_bits, "similarity_type": model.similarity_type,
+                "metrics": model.metrics}
+        if fhe != "execute":
+            from fheicp.params import params_for_bits
+            qp = model.model.quant_params
+            return self.store_keys(key_id, qp, params_for_bits(qp.msg_bits()), None, info)
         model.compile(X_train[:10], key_seed=key_seed)
         fm = model.model._fitted()
-        return self.store_keys(key_id, fm.qparams, fm.scheme, fm.engine.export_keys(),
-                               {"input_dim": model.input_dim, "n_bits": model.n_bits,
-                                "similarity_type": model.similarity_type, "metrics": model.metrics})
+        return self.store_keys(key_id, fm.qparams, fm.scheme, fm.engine.export_keys(), info)
 
-    def store_keys(self, key_id: str, qparams, scheme, keys: dict, info: dict) -> Dict[str, str]:
-        """Write <key_id>/compiled_model.enc (Fernet) + eval_keys.npz and make it current."""
+    def store_keys(self, key_id: str, qparams, scheme, keys: Optional[dict], info: dict) -> Dict[str, str]:
+        """Write <key_id>/compiled_model.enc (Fernet) + eval_keys.npz and make
+        it current; keys=None stores the quantized model alone (clear mode)."""
         key_path = self.key_dir / key_id
         key_path.mkdir(exist_ok=True)
         f = Fernet(self._get_master_key())
         model_data = dict(info)
-        model_data["compiled"] = True
-        model_data["fheicp"] = {
-            "format": FORMAT, "version": VERSION, "quant": qparams.to_dict(), "scheme": scheme.as_dict(),
-            "s_small": np.ascontiguousarray(keys["s_small"], dtype=np.uint64).tobytes(),
-            "s_big": np.ascontiguousarray(keys["s_big"], dtype=np.uint64).tobytes(),
-        }
+        model_data["compiled"] = keys is not None
+        model_data["fheicp"] = {"format": FORMAT, "version": VERSION, "quant": qparams.to_dict(),
+                                "scheme": scheme.as_dict()}
+        if keys is not None:
+            model_data["fheicp"]["s_small"] = np.ascontiguousarray(keys["s_small"], dtype=np.uint64).tobytes()
+            model_data["fheicp"]["s_big"] = np.ascontiguousarray(keys["s_big"], dtype=np.uint64).tobytes()
         encrypted_model = f.encrypt(pickle.dumps(model_data))
         model_file = key_path / "compiled_model.enc"
         model_file.write_bytes(encrypted_model)
         os.chmod(model_file, 0o600)
         eval_file = key_path / "eval_keys.npz"
-        tmp = str(eval_file) + ".tmp.npz"
-        np.savez(tmp, bsk=np.ascontiguousarray(keys["bsk"], dtype=np.uint64),
-                 ksk=np.ascontiguousarray(keys["ksk"], dtype=np.uint64))
-        os.replace(tmp, eval_file)
+        if keys is not None:
+            tmp = str(eval_file) + ".tmp.npz"
+            np.savez(tmp, bsk=np.ascontiguousarray(keys["bsk"], dtype=np.uint64),
+                     ksk=np.ascontiguousarray(keys["ksk"], dtype=np.uint64))
+            os.replace(tmp, eval_file)
         metadata = self._load_metadata()
         created = datetime.now().isoformat()
         metadata["keys"][key_id] = {"created": created, "path": str(key_path), "active": True,
                                     "model_file": str(model_file), "size_bytes": len(encrypted_model),
-                                    "eval_keys_file": str(eval_file)}
+                                    "eval_keys_file": str(eval_file) if keys is not None else None}
         metadata["current"] = key_id
         self.current_key_id = key_id
         self._save_metadata(metadata)
@@ -190,7 +204,8 @@ class FHEKeyManager:
         return data
 
     def load_key_material(self, key_id: Optional[str] = None):
-        """-> (QuantParams, SchemeParams, keys dict) of an fheicp key."""
+        """-> (QuantParams, SchemeParams, keys dict or None) of an fheicp key
+        (None: a clear-mode key, the quantized model without keys)."""
         from fheicp.model import QuantParams
         from fheicp.params import SchemeParams
         key_id, info = self._key_info(key_id)
@@ -200,6 +215,8 @@ class FHEKeyManager:
             raise ValueError(f"Key {key_id} holds no fheicp key material (written by the reference?)")
         if int(fh.get("version", 0)) > VERSION:
             raise ValueError(f"Key {key_id}: format version {fh['version']} is newer than supported {VERSION}")
+        if "s_small" not in fh or not info.get("eval_keys_file"):
+            return QuantParams.from_dict(fh["quant"]), SchemeParams(**fh["scheme"]), None
         with np.load(info["eval_keys_file"], allow_pickle=False) as z:
             keys = {"bsk": z["bsk"].copy(), "ksk": z["ksk"].copy()}
         keys["s_small"] = np.frombuffer(fh["s_small"], dtype=np.uint64).copy()
@@ -212,6 +229,8 @@ class FHEKeyManager:
         from fheicp.sklearn import LinearRegression
         data = self.load_model(key_id)
         qp, _, keys = self.load_key_material(key_id)
+        if keys is None:
+            raise ValueError("this key holds the quantized model only (generated with fhe != 'execute')")
         m = FHESimilarityModel(input_dim=len(qp.coef), n_bits=qp.n_bits,
                                similarity_type=data.get("similarity_type", "cosine"), device=device)
         m.metrics = dict(data.get("metrics", {}))

@@ -125,6 +125,14 @@ int fhe_phase_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, uint64_t*
  * ct: B x D big ciphertexts (row-major), d_w: D int64 (device). */
 int fhe_linear_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                      uint64_t* d_out, void* stream);
+/* fhe_encrypt_batch of the B x D messages d_qx (ciphertext b*D + j uses
+ * stream id id0 + b*D + j) followed by fhe_linear_batch, fused: the input
+ * ciphertexts are never written (mod-2^64 linearity makes the output
+ * bit-identical to the two calls). The single-party form of the reference's
+ * predict(fhe="execute") (fhe_similarity.py:151): client encryption and the
+ * server's leveled dot product in one pass; d_out: B x (kN+1). */
+int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
+                             const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream);
 /* big -> small key switch of (ct << shift) + add_body (shift/add used by the
  * bit extraction; pass 0, 0 for a plain key switch) */
 int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
@@ -165,6 +173,25 @@ int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_r
 int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t base, uint64_t step,
                       int32_t log_slots, uint64_t* d_out, void* stream);
 
+/* Programmable bootstrap with an arbitrary table (SURVEY.md §8b
+ * fhe_pbs_batch(ctx, ct_in, B, const int64* lut, ct_out)): the input small
+ * LWE encrypts a message m in [0, 2^lut_bits) at 2^(63 - lut_bits) (one
+ * padding bit); the output big LWE encrypts d_lut[m] (a signed msg_bits-bit
+ * value) at Delta = 2^(64 - msg_bits). The test vector is built on the device
+ * from d_lut (2^lut_bits int64, device memory): box m covers the input phases
+ * within half a box of m * 2^(63 - lut_bits). 0 <= lut_bits <= log2(N) - 1;
+ * the caller keeps the input noise (after key and modulus switching) inside
+ * half a box. */
+int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const int64_t* d_lut, int32_t lut_bits,
+                        uint64_t* d_out, void* stream);
+/* The encrypted decision of batch_operations.py:278 (score >= min_similarity
+ * <=> acc >= T, SURVEY.md §8b fhe_threshold_batch): d_ct_acc holds big LWEs of
+ * msg_bits-bit accumulators (not modified); d_bit receives the encryption of
+ * [acc >= T] at 2^63 (fhe_decrypt_bits_batch). acc - T must fit msg_bits
+ * bits. fhe_sign_pbs_count(params) key switches + bootstraps per ciphertext. */
+int fhe_threshold_batch(fhe_ctx* ctx, const uint64_t* d_ct_acc, int64_t count, int64_t T, uint64_t* d_bit,
+                        void* stream);
+
 /* ---- fused compare / search ------------------------------------------------
  * One call per batch of B (query, document) pairs — the batched replacement
  * of the per-document loop at batch_operations.py:268-279 and of
@@ -175,7 +202,9 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
  *   q_x @ q_w - zp*sum(q_w) + q_b; read from the leveled ciphertext like the
  *   reference's leveled circuit), d_below[b] = 1 iff acc < T (the decrypted
  *   bootstrapped threshold bit; acc >= T <=> score >= min_similarity).
- * Uses context-owned workspace (grown on demand; not graph-capturable). */
+ * Uses context-owned workspace of ~8 * B * (2(kN+1) + n + 2) bytes (grown on
+ * demand; not graph-capturable): the encryption is fused into the linear step
+ * (fhe_encrypt_linear_batch), so D does not enter the footprint. */
 int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                       int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream);
 
@@ -249,10 +278,17 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
  * what it read. */
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
-/* Development aid: 4 x 16 s_memtime phase stamps of one wave of the v4 blind
- * rotation, then 2048 x {start, end, HW_ID} per workgroup (s_memrealtime),
- * recorded only when FHEICP_V4_DBG=128 (tools/prof_br.py --stamps);
- * h_out holds 64 + 6144 words. */
+/* The kernel last launched for that bucket, as rocprofv3 names it (e.g.
+ * "k_blind_rotate_v4<2, true, 0, 4, false>", "k_blind_rotate_mw<fhei::V2, 2, 2>",
+ * "k_keyswitch_mfma"); "" before any launch. Not reset by fhe_profile_read. */
+int fhe_profile_kernel_name(fhe_ctx* ctx, const char* kernel, char* h_buf, size_t len);
+/* "libfheicp gfx950 ab=0" for the shipped build; ab=1 for A/B builds
+ * (tools/build_variant.sh -DFHEICP_AB: extra v4 shapes, v3, timing kernels). */
+const char* fhe_build_info(void);
+/* Development aid (A/B builds only; FHE_E_STATE otherwise): 4 x 16 s_memtime
+ * phase stamps of one wave of the v4 blind rotation, then 2048 x {start, end,
+ * HW_ID} per workgroup (s_memrealtime), recorded only when FHEICP_V4_DBG=128
+ * (tools/prof_br.py --stamps); h_out holds 64 + 6144 words. */
 int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out);
 
 #ifdef __cplusplus

@@ -424,11 +424,27 @@ static uint32_t modswitch(uint64_t a, int log2N2) {
   return (uint32_t)((((a >> (63 - log2N2)) + 1) >> 1) & ((1ull << log2N2) - 1));
 }
 
-/* Test vector TV_j = base + (j >> shift) * step, j in [0, N), extended
- * negacyclically (a staircase; step 0 = constant). */
-typedef struct { uint64_t base, step; int shift; } tv_desc;
+/* Test vector TV_j, j in [0, N), extended negacyclically: a staircase
+ * base + (j >> shift) * step (step 0 = constant), or, with a table (lut !=
+ * NULL, fhe_pbs_table_batch), box m = (j + half box) >> log_box holding
+ * lut[m] * delta, and the top half box holding -lut[0] * delta (its
+ * negacyclic image is the half box just below phase 0). */
+typedef struct {
+  uint64_t base, step;
+  int shift;
+  const int64_t* lut;
+  int lut_count, log_box;
+  uint64_t delta;
+} tv_desc;
 static uint64_t tv_at(const tv_desc* tv, uint32_t idx, int N) {
-  const uint64_t v = tv->base + (uint64_t)((idx & (uint32_t)(N - 1)) >> tv->shift) * tv->step;
+  const uint32_t j = idx & (uint32_t)(N - 1);
+  uint64_t v;
+  if (tv->lut) {
+    const uint32_t m = (j + (1u << (tv->log_box - 1))) >> tv->log_box;
+    v = m < (uint32_t)tv->lut_count ? (uint64_t)tv->lut[m] * tv->delta : (uint64_t)0 - (uint64_t)tv->lut[0] * tv->delta;
+  } else {
+    v = tv->base + (uint64_t)(j >> tv->shift) * tv->step;
+  }
   return idx < (uint32_t)N ? v : (uint64_t)0 - v;
 }
 
@@ -484,7 +500,7 @@ void ref_pbs_const(const ref_params* P, const uint64_t* bsk, const uint64_t* sma
 #pragma omp parallel
   {
     uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
-    const tv_desc d = {tv, 0, 0};
+    const tv_desc d = {tv, 0, 0, NULL, 0, 0, 0};
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c)
       pbs1(P, bsk, small + (size_t)c * (P->n + 1), &d, out + (size_t)c * (P->k * P->N + 1), work);
@@ -499,7 +515,24 @@ void ref_pbs_lut(const ref_params* P, const uint64_t* bsk, const uint64_t* small
 #pragma omp parallel
   {
     uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
-    const tv_desc d = {base, step, ilog2(P->N) - log_slots};
+    const tv_desc d = {base, step, ilog2(P->N) - log_slots, NULL, 0, 0, 0};
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c)
+      pbs1(P, bsk, small + (size_t)c * (P->n + 1), &d, out + (size_t)c * (P->k * P->N + 1), work);
+    free(work);
+  }
+}
+
+/* Bootstrap with a table test vector (fhe_pbs_table_batch semantics): the
+ * input encrypts m in [0, 2^lut_bits) at 2^(63 - lut_bits), the output lut[m]
+ * at 2^(64 - msg_bits). */
+void ref_pbs_table(const ref_params* P, const uint64_t* bsk, const uint64_t* small, int64_t count, const int64_t* lut,
+                   int lut_bits, uint64_t* out) {
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(P));
+    tv_desc d = {0, 0, 0, lut, 1 << lut_bits, ilog2(P->N) - lut_bits, 0};
+    d.delta = 1ull << (64 - P->msg_bits);
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c)
       pbs1(P, bsk, small + (size_t)c * (P->n + 1), &d, out + (size_t)c * (P->k * P->N + 1), work);
@@ -540,7 +573,7 @@ void ref_bit_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* k
         sh[Wb - 1] += 1ull << 62;
         keyswitch1(P, ksk, sh, sm);
         const uint64_t tv = 1ull << (63 - Pb + i);
-        const tv_desc d = {tv, 0, 0};
+        const tv_desc d = {tv, 0, 0, NULL, 0, 0, 0};
         pbs1(P, bsk, sm, &d, ob, work);
         for (int t = 0; t < Wb - 1; ++t) ob[t] = (uint64_t)0 - ob[t];
         ob[Wb - 1] = tv - ob[Wb - 1];
@@ -580,11 +613,22 @@ static void sign_round(const ref_params* P, const uint64_t* bsk, const uint64_t*
  * main rounds keeping every round at 9.2 sigma. */
 static double tu_var(int b) { return (ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
 
+/* Bootstrap output variance: GGSW key noise + gadget rounding (counted over
+ * all n steps) + the f64 FFT's arithmetic error per step and output
+ * coefficient, C_FFT * rows * N * B^2 / 144 * 2^-106 (the product's variance
+ * times the f64 unit roundoff squared; C_FFT = 16 bounds the 11.6-13.8
+ * measured on every MI355X kernel instance, tests/test_gpu_noise.py), plus
+ * the 2^32 output rounding of the 32-bit-accumulator kernels (L*beta <= 31);
+ * both key-weighted like the gadget rounding. */
+#define C_FFT 16.0
 static double pbs_variance(const ref_params* P, int base_log, int L) {
   const double beta = ldexp(1.0, base_log);
-  const double key = (double)P->n * L * (P->k + 1) * P->N * (beta * beta + 2) / 12.0 * tu_var(P->glwe_noise_bits) /
-                     ldexp(1.0, 128);
-  return key + (double)P->n * (1 + P->k * P->N / 2.0) / (12.0 * pow(beta, 2.0 * L));
+  const double rows = (double)L * (P->k + 1) * P->N;
+  const double key = (double)P->n * rows * (beta * beta + 2) / 12.0 * tu_var(P->glwe_noise_bits) / ldexp(1.0, 128);
+  const double steps = (double)P->n * (1 + P->k * P->N / 2.0);
+  double arith = C_FFT * rows * beta * beta / 144.0 * ldexp(1.0, -106);
+  if (base_log * L <= 31) arith += ldexp(1.0, -64) / 12.0;
+  return key + steps / (12.0 * pow(beta, 2.0 * L)) + steps * arith;
 }
 static double fixed_variance(const ref_params* P) {
   const double bk = ldexp(1.0, P->ks_base_log);
@@ -694,10 +738,10 @@ static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int
   const ref_params* Pr;
   const uint64_t* bk;
   const int Pb = g->P->msg_bits, lgN = ilog2(g->P->N);
-  const tv_desc hi = {1ull << (62 - Pb + b + c), 0, 0};
+  const tv_desc hi = {1ull << (62 - Pb + b + c), 0, 0, NULL, 0, 0, 0};
   sched_next(g, &Pr, &bk);
   sign_round(Pr, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &hi, 1, sh, sm, ob, work);
-  const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - (c - 1)};
+  const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - (c - 1), NULL, 0, 0, 0};
   sched_next(g, &Pr, &bk);
   sign_round(Pr, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &lo, 2, sh, sm, ob, work);
 }
@@ -738,7 +782,7 @@ void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t
       const uint64_t* bk;
       if (Pb < 4) {
         for (int i = 0; i < Pb; ++i) {
-          const tv_desc t = {1ull << (63 - Pb + i), 0, 0};
+          const tv_desc t = {1ull << (63 - Pb + i), 0, 0, NULL, 0, 0, 0};
           sign_round(P, bsk, ksk, cv, Pb - 1 - i, 1ull << 62, &t, 1, sh, sm, ob, work);
         }
       } else {
@@ -750,11 +794,11 @@ void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t
           b = m;
         }
         for (; b < m; ++b) {
-          const tv_desc t = {1ull << (63 - Pb + b), 0, 0};
+          const tv_desc t = {1ull << (63 - Pb + b), 0, 0, NULL, 0, 0, 0};
           sched_next(&g, &Pr, &bk);
           sign_round(Pr, bk, ksk, cv, Pb - b - 1, 1ull << 62, &t, 1, sh, sm, ob, work);
         }
-        const tv_desc top = {1ull << 62, 0, 0};
+        const tv_desc top = {1ull << 62, 0, 0, NULL, 0, 0, 0};
         sched_next(&g, &Pr, &bk);
         sign_round(Pr, bk, ksk, cv, 0, 1ull << (63 - d), &top, 1, sh, sm, ob, work);
       }

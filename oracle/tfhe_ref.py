@@ -59,6 +59,7 @@ def lib():
         L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
         L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_pbs_table.argtypes = [P, u64p, u64p, C.c_int64, i64p, C.c_int, u64p]
         L.ref_sign_extract3.argtypes = [P, u64p, u64p, u64p, u64p, u64p, C.c_int64, u64p]
         L.ref_sign_plan.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.ref_sign_precise_rounds.argtypes = [P]; L.ref_sign_precise_rounds.restype = C.c_int
@@ -213,6 +214,25 @@ class RefTFHE:
         lib().ref_pbs_lut(C.byref(self.P), u64(self.bsk), u64(small), cnt, C.c_uint64(base), C.c_uint64(step),
                           int(log_slots), u64(out))
         return out
+
+    def pbs_table(self, small: np.ndarray, lut, lut_bits: int) -> np.ndarray:
+        """fhe_pbs_table_batch restated (oracle/tfhe_ref.c ref_pbs_table)."""
+        small = np.ascontiguousarray(small, dtype=np.uint64)
+        lut = np.ascontiguousarray(lut, dtype=np.int64)
+        assert lut.size == 1 << lut_bits
+        cnt = small.size // (self.n + 1)
+        out = np.zeros((cnt, self.big + 1), np.uint64)
+        lib().ref_pbs_table(C.byref(self.P), u64(self.bsk), u64(small), cnt, i64(lut), int(lut_bits), u64(out))
+        return out
+
+    def threshold(self, ct_acc: np.ndarray, T: int) -> np.ndarray:
+        """fhe_threshold_batch restated: the sign extraction of acc - T
+        (trivially subtracted), then 1 - sign: [acc >= T] at 2^63."""
+        cv = np.array(ct_acc, dtype=np.uint64, copy=True, order="C").reshape(-1, self.big + 1)
+        cv[:, -1] -= np.uint64((int(T) << (64 - self.params["msg_bits"])) % (1 << 64))
+        bit = (np.uint64(0) - self.sign_extract(cv)).astype(np.uint64)
+        bit[:, -1] += np.uint64(1 << 63)
+        return bit
 
     def sign_extract(self, ct_v: np.ndarray) -> np.ndarray:
         """fhe_sign_batch restated: encryption of [v < 0] at 2^63 (ct_v copied)."""

@@ -96,3 +96,24 @@ def test_fast_gadget_validation_and_host_calls():
     buf = (C.c_uint64 * 1)()
     assert L.fhe_export_fast_bsk(h, 1, buf) == -2
     L.fhe_ctx_destroy(h)
+
+
+def test_build_info_and_kernel_names_on_host_context():
+    """The shipped build says ab=0; a host-only context has no launched
+    kernels (empty names), rejects unknown buckets, and the table bootstrap
+    and threshold entries refuse without a device."""
+    L = _lib.lib()
+    assert L.fhe_build_info() == b"libfheicp gfx950 ab=0"
+    assert not _lib.ab_build()
+    P = _lib.params_struct(params_for_bits(16).as_dict())
+    h = C.c_void_p()
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
+    buf = C.create_string_buffer(64)
+    for k in (b"blind_rotate", b"blind_rotate_main", b"blind_rotate_fast", b"blind_rotate_fast2", b"keyswitch"):
+        assert L.fhe_profile_kernel_name(h, k, buf, 64) == 0 and buf.value == b""
+    assert L.fhe_profile_kernel_name(h, b"nope", buf, 64) == -1
+    assert L.fhe_profile_kernel_name(h, b"keyswitch", None, 64) == -1
+    assert L.fhe_pbs_table_batch(h, None, 0, None, 4, None, None) == -2
+    assert L.fhe_threshold_batch(h, None, 0, 0, None, None) == -2
+    assert L.fhe_debug_v4_stamps(h, buf) == -2
+    L.fhe_ctx_destroy(h)

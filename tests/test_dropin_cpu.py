@@ -216,7 +216,7 @@ class _Keys:
 def _processor(tmp_path, **cfg):
     from batch_operations import BatchConfig, BatchProcessor
     from encrypted_storage import EncryptedDocumentStore
-    c = BatchConfig(**{"fhe": "disable", "input_dim": 16, "n_bits": 6, "seed": 21, "show_progress": False, **cfg})
+    c = BatchConfig(**{"fhe": "disable", "input_dim": 16, "n_bits": 6, "seed": 21, "show_progress": False, "key_manager_default": False, **cfg})
     return BatchProcessor(embedder=_Embedder(), reducer=_Reducer(), storage=EncryptedDocumentStore(str(tmp_path)),
                           config=c)
 

@@ -109,7 +109,7 @@ def test_batch_processor_ciphertext_store(tmp_path, need_gpu):
     from batch_operations import BatchConfig, BatchProcessor
     from encrypted_storage import CIPHERTEXT_VERSION, EncryptedDocumentStore
     cfg = BatchConfig(input_dim=16, n_bits=6, seed=3, key_seed=8, store_ciphertexts=True,
-                      corpus_path=str(tmp_path / "corpus.npz"), batch_size=100)
+                      corpus_path=str(tmp_path / "corpus.npz"), batch_size=100, key_manager_default=False)
     store = EncryptedDocumentStore(str(tmp_path / "docs"))
     bp = BatchProcessor(storage=store, config=cfg)
     q, docs = Q.make_corpus(16, 300, seed=23)

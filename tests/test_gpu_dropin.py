@@ -64,7 +64,7 @@ def test_processor_encrypted_search_matches_oracle(need_gpu, tmp_path):
     from batch_operations import BatchConfig, BatchProcessor
     from encrypted_storage import EncryptedDocument, EncryptedDocumentStore
     cfg = BatchConfig(fhe="execute", input_dim=16, n_bits=6, seed=40, key_seed=41, search_chunk=128,
-                      show_progress=False)
+                      show_progress=False, key_manager_default=False)
     p = BatchProcessor(storage=EncryptedDocumentStore(str(tmp_path)), config=cfg)
     q, docs = Q.make_corpus(16, 500, seed=13)
     docs[7] = docs[300]

@@ -1,0 +1,72 @@
+"""GPU: the bootstrap noise that "bit-exact" rests on, per shipped
+blind-rotation instance.
+
+Every decision of the sign extraction is exact only while the noise stays
+inside its margin (>= 9.2 sigma of the model, p_fail <= 2^-64 per bootstrap;
+DESIGN.md §3.5). Sampling a thousand compares cannot show that, so for each
+kernel instance the parameter table can select (v4 32-bit accumulators at
+(15,2) and (23,1), v4 64-bit at (12,3), v2 at levels 4..8) this measures the
+output noise of >= 4096 bootstraps on the real parameters and checks it
+against the model (fheicp.params._variances, the same formula as fheicp.hip
+and oracle/tfhe_ref.c), and checks a few output phases against the exact
+oracle's bootstrap of the same inputs.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from fheicp.engine import Engine, u64
+from fheicp.params import SchemeParams, _variances
+
+pytestmark = pytest.mark.gpu
+
+# (base_log, level) -> the instantiation fhe_profile_kernel_name reports
+INSTANCES = {
+    (15, 2): "k_blind_rotate_v4<2, true, 0, 4, false>",
+    (23, 1): "k_blind_rotate_v4<1, true, 0, 4, false>",
+    (12, 3): "k_blind_rotate_v4<3, false, 0, 2, false>",
+    (10, 4): "k_blind_rotate_mw<fhei::V2, 2, 2>",
+    (8, 5): "k_blind_rotate_mw<fhei::V2, 2, 2>",
+    (7, 6): "k_blind_rotate_mw<fhei::V2, 2, 2>",
+    (6, 7): "k_blind_rotate_mw<fhei::V2, 2, 2>",
+    (5, 8): "k_blind_rotate_mw<fhei::V2, 2, 2>",
+}
+COUNT = 4096
+TV = 1 << 61
+
+
+def signed(x):
+    return np.asarray(x, dtype=np.uint64).view(np.int64)
+
+
+@pytest.mark.parametrize("gadget", list(INSTANCES))
+def test_bootstrap_noise_vs_model(need_gpu, oracle_lib, gadget):
+    beta, lvl = gadget
+    prm = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=16)
+    eng = Engine(prm, 0)
+    eng.keygen(5000 + 10 * beta + lvl)
+    # inputs at phase +-2^62: far from the 0 / 2^63 boundaries, so the key
+    # and modulus switch noise never flips the rotation's half of the torus
+    sgn = np.where(np.arange(COUNT) % 2 == 0, 1, -1).astype(np.int64)
+    v = sgn * (1 << 14)
+    small = eng.keyswitch(eng.encrypt(v, seed=17), 0, 0)
+    eng.profile(True)
+    out = eng.pbs(small, TV)
+    eng.profile(False)
+    assert eng.kernel_name("blind_rotate_main") == INSTANCES[gadget]
+    assert eng.profile_read("blind_rotate_main")["items"] == COUNT
+    ph = signed(u64(eng.phase(out)))
+    err = (ph - sgn * TV).astype(np.float64) / 2.0 ** 64
+    sigma = float(np.sqrt(np.mean(err ** 2)))   # RMS: a bias would count too
+    sigma_model = math.sqrt(_variances(prm)[0])
+    print(f"gadget {gadget}: sigma 2^{math.log2(sigma):.2f}, model 2^{math.log2(sigma_model):.2f}, "
+          f"max |err| {np.abs(err).max() / sigma_model:.2f} model sigmas")
+    assert sigma <= 1.1 * sigma_model
+    # the same bootstraps in the exact oracle: phases agree to noise level
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 5000 + 10 * beta + lvl)
+    sm = u64(small)[:2]
+    ph_ref = signed(ref.phase(ref.pbs_const(sm, TV)))
+    assert np.abs(ph[:2] - ph_ref).max() < 8 * sigma_model * 2.0 ** 64
+    assert np.array_equal(ph_ref > 0, sgn[:2] > 0)
+    eng.close()

@@ -176,10 +176,19 @@ def test_topk_matches_stable_sort(need_gpu):
         assert np.all(got_i[len(exp):] == -1)
 
 
+def _need_ab():
+    from fheicp import _lib
+    if not _lib.ab_build():
+        pytest.skip("A/B-only kernel shape: run with FHEICP_LIB=<tools/build_variant.sh ab -DFHEICP_AB build>")
+
+
 @pytest.mark.parametrize("variant", ["2", "3"])
 def test_bit_extract_real_params_other_kernels(need_gpu, oracle_lib, monkeypatch, variant):
-    """The A/B blind-rotation kernels (FHEICP_BR_VARIANT=2: two waves per
-    ciphertext, 3: four) give the same results as the default (v4)."""
+    """The other blind-rotation kernels (FHEICP_BR_VARIANT=2: two waves per
+    ciphertext, shipped for gadget levels >= 4; 3: four, A/B builds only)
+    give the same results as the default (v4)."""
+    if variant == "3":
+        _need_ab()
     monkeypatch.setenv("FHEICP_BR_VARIANT", variant)
     eng = Engine(REAL16, 0)
     eng.keygen(777)
@@ -354,6 +363,8 @@ def test_v4_workgroup_shapes(need_gpu, monkeypatch, g, fl):
     or per-ciphertext LDS hand-offs FHEICP_V4_FL) gives the exact sign and
     refreshed value on the real parameters, with a batch that is not a multiple
     of the workgroup (B = 1023: the last workgroup runs padding ciphertexts)."""
+    if (g, fl) != ("4", "0"):
+        _need_ab()
     monkeypatch.setenv("FHEICP_V4_G", g)
     monkeypatch.setenv("FHEICP_V4_FL", fl)
     eng = Engine(REAL16, 0)
@@ -366,3 +377,70 @@ def test_v4_workgroup_shapes(need_gpu, monkeypatch, g, fl):
     ref_ct, sign2 = eng.bit_extract(eng.encrypt(v[:64], seed=25))
     assert np.array_equal(eng.decrypt(ref_ct).cpu().numpy(), v[:64])
     eng.close()
+
+
+def test_pbs_table_every_value_real(real):
+    """fhe_pbs_table_batch on the real parameters: an arbitrary 3-bit table
+    (a requantisation-like map with signed outputs) over every input, 64
+    times each, decrypts exactly; a 4-bit table over every input decrypts
+    exactly and its phases track the oracle's ref_pbs_table."""
+    eng, ref = real
+    P = eng.msg_bits
+    try:
+        for lut_bits, reps in ((3, 64), (4, 1)):
+            M = 1 << lut_bits
+            lut = np.random.default_rng(lut_bits).integers(-(2 ** (P - 1)), 2 ** (P - 1), M)
+            lut[0], lut[-1] = -(2 ** (P - 1)), 2 ** (P - 1) - 1
+            m = np.tile(np.arange(M, dtype=np.int64), reps)
+            eng.set_msg_bits(lut_bits + 1)          # input encoding: padding bit + lut_bits
+            small = eng.keyswitch(eng.encrypt(m, seed=70 + lut_bits), 0, 0)
+            eng.set_msg_bits(P)
+            out = eng.pbs_table(small, lut, lut_bits)
+            assert np.array_equal(eng.decrypt(out).cpu().numpy(), lut[m])
+            if lut_bits == 4:
+                ref.with_msg_bits(P)
+                o_ref = ref.pbs_table(u64(small)[:4], lut, lut_bits)
+                assert np.array_equal(ref.decrypt_ints(o_ref), lut[m[:4]])
+                d = signed(u64(eng.phase(out[:4].contiguous())) - ref.phase(o_ref))
+                assert np.abs(d).max() < 2 ** 48
+    finally:
+        eng.set_msg_bits(P)
+
+
+def test_threshold_batch_real(real):
+    """fhe_threshold_batch: [acc >= T] (batch_operations.py:278) for
+    accumulators at and around T and at the ends of the 16-bit range; the
+    accumulator ciphertext is left unchanged; the oracle's restatement
+    decrypts to the same bits."""
+    eng, ref = real
+    P = eng.msg_bits
+    T = 1234
+    h = 2 ** (P - 2)
+    acc = np.concatenate([[T - 2, T - 1, T, T + 1, -h, h - 1, 0, -1],
+                          np.random.default_rng(77).integers(-h, h, 504)]).astype(np.int64)
+    ct = eng.encrypt(acc, seed=78)
+    before = u64(ct).copy()
+    bit = eng.threshold(ct, T)
+    assert np.array_equal(u64(ct), before)
+    assert np.array_equal(eng.decrypt_bits(bit).cpu().numpy(), (acc >= T).astype(np.int64))
+    b_ref = ref.threshold(u64(ct)[:4], T)
+    assert np.array_equal(ref.decrypt_bits(b_ref), (acc[:4] >= T).astype(np.int64))
+
+
+@pytest.mark.parametrize("which", ["toy", "real"])
+def test_encrypt_linear_fused_bit_exact(which, request):
+    """fhe_encrypt_linear_batch (the fused client encryption + leveled dot of
+    fhe_compare_batch) is bit-identical to fhe_encrypt_batch followed by
+    fhe_linear_batch, and to the oracle's encrypt + linear, including a
+    feature count that is not a multiple of anything (D = 37)."""
+    eng, ref = request.getfixturevalue(which)
+    rng = np.random.default_rng(11)
+    for B, D in ((5, 37), (64, 16)):
+        x = rng.integers(-32, 32, (B, D))
+        w = rng.integers(-127, 128, D)
+        cst = int(rng.integers(-1000, 1000))
+        fused = u64(eng.encrypt_linear(x, w, cst, seed=8, id0=77))
+        two = u64(eng.linear(eng.encrypt(x, seed=8, id0=77), B, D, w, cst))
+        assert np.array_equal(fused, two)
+        lin_ref = ref.linear(ref.encrypt_ints(x, seed=8, id0=77), B, D, w, cst)
+        assert np.array_equal(fused, lin_ref)

@@ -209,3 +209,32 @@ def test_sign_extract_three_gadgets(oracle_lib, P, d):
                         np.random.default_rng(P).integers(-h, h, 120)]).astype(np.int64)
     sign = r.sign_extract(r.encrypt_ints(v, seed=300 + P))
     assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
+
+
+@pytest.mark.parametrize("lut_bits", [1, 3, 4])
+def test_oracle_pbs_table_every_value(oracle_lib, lut_bits):
+    """ref_pbs_table (the restatement of fhe_pbs_table_batch) on the TOY set:
+    an arbitrary signed table, every input message, the output decrypts to
+    lut[m] at the context's msg_bits."""
+    from dataclasses import replace
+    P_out = 8
+    prm = replace(TOY, msg_bits=lut_bits + 1)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 99)
+    M = 1 << lut_bits
+    m = np.arange(M, dtype=np.int64)
+    lut = np.random.default_rng(lut_bits).integers(-(2 ** (P_out - 1)), 2 ** (P_out - 1), M)
+    small = ref.keyswitch(ref.encrypt_ints(m, seed=5))
+    ref.with_msg_bits(P_out)
+    out = ref.pbs_table(small, lut, lut_bits)
+    assert np.array_equal(ref.decrypt_ints(out), lut)
+
+
+def test_oracle_threshold_restatement(oracle_lib):
+    """RefTFHE.threshold (fhe_threshold_batch): [acc >= T] for accumulators
+    around T and at the ends of the P-bit range, on the TOY set."""
+    P = TOY.msg_bits
+    ref = oracle_lib.RefTFHE(TOY.as_dict(), 7)
+    T = 5
+    acc = np.array([-(2 ** (P - 2)), T - 2, T - 1, T, T + 1, 2 ** (P - 2)], dtype=np.int64)
+    bit = ref.threshold(ref.encrypt_ints(acc, seed=3), T)
+    assert np.array_equal(ref.decrypt_bits(bit), (acc >= T).astype(np.int64))

@@ -73,8 +73,8 @@ def test_fast_gadget_plan():
     F, F2 = (15, 2), (23, 1)
     want = {4: (F2, None, (4, 0, 1)), 9: (F2, None, (4, 0, 4)), 12: (F2, None, (4, 1, 5)),
             16: (F2, None, (4, 3, 7)), 17: (F2, None, (3, 5, 11)), 18: (F, F2, (4, 1, 5)),
-            19: (F, F2, (4, 1, 5)), 20: (F, F2, (4, 2, 5)), 21: (F, F2, (3, 3, 7)), 22: (F, F2, (4, 3, 7)),
-            23: (F, F2, (3, 4, 9)), 24: (F, F2, (4, 4, 7)), 25: (F, F2, (3, 5, 10)), 26: (F, F2, (3, 6, 11)),
+            19: (F, F2, (4, 1, 5)), 20: (F, F2, (4, 2, 5)), 21: (F, F2, (3, 3, 7)), 22: (F, F2, (3, 3, 8)),
+            23: (F, F2, (3, 4, 9)), 24: (F, F2, (3, 5, 9)), 25: (F, F2, (3, 5, 10)), 26: (F, F2, (3, 6, 11)),
             27: (F, F2, (3, 7, 11))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Per-kernel PMC figures of the bench's blind-rotation kernels, keyed on the
+sha256 of the libfheicp.so they were measured on (bench.py reads them only
+for that exact build).
+
+Inputs: rocprofv3 counter_collection.csv files of separate --pmc passes over
+`bench.py --steps 1 --warmup 0 --no-cpu-baseline` (tools/pmc_bench.sh):
+  f64   SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU
+  fetch FETCH_SIZE
+  write WRITE_SIZE
+and the kernel-trace csv of the same command for the per-launch durations.
+Recipe (MI355X_MICROARCH.md, HBM/rocprofv3): SQ_INSTS_* count wave64
+instructions, so f64 FLOPs = 64 x (2 FMA + ADD + MUL); FETCH_SIZE/WRITE_SIZE
+are KiB from separate passes and gfx950's FETCH_SIZE counts half the bytes of
+wide coalesced reads: hbm_bytes = (2 FETCH_SIZE + WRITE_SIZE) x 1024.
+Usage: br_pmc.py --lib LIB --cts N --f64 CSV --fetch CSV --write CSV [--trace CSV] --out JSON
+"""
+import argparse
+import collections
+import csv
+import hashlib
+import json
+
+
+def kname(s: str) -> str:
+    s = s.strip()
+    if s.startswith("void "):
+        s = s[5:]
+    return s.split("(")[0]
+
+
+def per_kernel(path, match=("k_blind_rotate", "k_keyswitch")):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        n = kname(r["Kernel_Name"])
+        if any(m in n for m in match):
+            acc[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {n: {c: (sum(v) / len(v), len(v)) for c, v in cs.items()} for n, cs in acc.items()}
+
+
+def trace_ms(path):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        n = kname(r["Kernel_Name"])
+        d[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+    return {n: (sum(v) / len(v), len(v)) for n, v in d.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("--cts", type=int, required=True, help="ciphertexts per launch of the measured command")
+    ap.add_argument("--f64", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--trace", default="")
+    ap.add_argument("--command", default="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    f64, fetch, write = per_kernel(a.f64), per_kernel(a.fetch), per_kernel(a.write)
+    tr = trace_ms(a.trace) if a.trace else {}
+    out = {"lib_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(), "command": a.command,
+           "cts_per_launch": a.cts, "kernels": {}}
+    for n, c in f64.items():
+        fma, add, mul = (c.get(f"SQ_INSTS_VALU_{x}_F64", (0.0, 0))[0] for x in ("FMA", "ADD", "MUL"))
+        e = {"cts_per_launch": a.cts, "launches": c.get("SQ_INSTS_VALU_FMA_F64", (0, 0))[1],
+             "f64_insts_per_launch": {"fma": fma, "add": add, "mul": mul},
+             "valu_insts_per_launch": c.get("SQ_INSTS_VALU", (0.0, 0))[0],
+             "f64_flops_per_launch": 64.0 * (2 * fma + add + mul)}
+        if n in fetch and n in write:
+            fk, wk = fetch[n]["FETCH_SIZE"][0], write[n]["WRITE_SIZE"][0]
+            e.update(fetch_size_kib=fk, write_size_kib=wk, hbm_bytes_per_launch=(2 * fk + wk) * 1024)
+        if n in tr:
+            e["avg_launch_ms"], e["trace_launches"] = tr[n]
+        out["kernels"][n] = e
+    s = json.dumps(out, indent=1)
+    open(a.out, "w").write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()

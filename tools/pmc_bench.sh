@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC passes over the headline bench command (one per counter group, each its
+# own run, as the gfx950 recipe requires) and the per-kernel summary bench.py
+# reads: gpurun_out/pmc_bench/br_pmc.json (copy it to profiles/br_pmc.json).
+# Extra bench.py arguments (another config) go in $BENCH_ARGS; $CTS is the
+# ciphertexts per launch (the documents per GPU of that run).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/pmc_bench; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
+CMD="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}"
+csvof() { ls "$1"/*counter_collection.csv "$1"/*/*counter_collection.csv 2>/dev/null | head -n1; }
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU \
+  -d "$OUT/f64" -o pmc --output-format csv -- python3 $CMD > "$OUT/f64.log" 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc --output-format csv -- python3 $CMD > "$OUT/fetch.log" 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o pmc --output-format csv -- python3 $CMD > "$OUT/write.log" 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $CMD > "$OUT/trace.log" 2>&1 || exit 1
+python3 tools/br_pmc.py --lib fhe-icp_amd/fheicp/libfheicp.so --cts "${CTS:-1024}" --f64 "$(csvof "$OUT/f64")" \
+  --fetch "$(csvof "$OUT/fetch")" --write "$(csvof "$OUT/write")" \
+  --trace "$(ls "$OUT"/trace/*kernel_trace.csv "$OUT"/trace/*/*kernel_trace.csv 2>/dev/null | head -n1)" \
+  --command "python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}" --out "$OUT/br_pmc.json" > "$OUT/br_pmc.log" 2>&1
