@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Encrypted-compare throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): one query against a shard of 1024
-documents per GPU, 16-dim features, n_bits = 6. One step = one pass of the
-whole encrypted path over the shard, all on the GPU:
+Workload at N = 1 (BASELINE.json configs[1], the metric's config): one query
+against 1024 documents, 16-dim features, n_bits = 6. At N > 1 (or with
+--workload c4) the north-star scaling workload, configs[3]: a 100k-document
+search, 16-dim, n_bits = 6, the corpus sharded over the ranks in contiguous
+global index ranges (strong scaling: the total is fixed). One step = one pass
+of the whole encrypted path over each rank's shard, all on the GPU:
     pair features + quantize -> encrypt (D LWEs per pair) -> leveled dot
     product with the quantized weights -> decrypt the accumulator ->
     P-round exact bit extraction (P key switches + P bootstraps per pair)
@@ -47,7 +50,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=1024, help="documents per GPU (shard size)")
+    ap.add_argument("--workload", choices=("auto", "c2", "c4"), default="auto",
+                    help="c2: configs[1], --docs per GPU (weak); c4: configs[3], --total-docs over all ranks "
+                         "(strong); auto: c2 at N=1, c4 at N>1")
+    ap.add_argument("--docs", type=int, default=1024, help="documents per GPU (c2 shard size)")
+    ap.add_argument("--total-docs", type=int, default=100_000, help="documents over all ranks (c4)")
     ap.add_argument("--dim", type=int, default=16)
     ap.add_argument("--n-bits", type=int, default=6)
     ap.add_argument("--top-k", type=int, default=10)
@@ -86,15 +93,25 @@ def build_model(args):
     return FheLinearModel.fit(X, y, n_bits=args.n_bits)
 
 
-def shard(args, rank):
+def shard(args, rank, world=1):
+    """(query, this rank's documents, global index of its first document).
+    c2: every rank draws its own --docs documents (weak scaling); c4: one
+    global corpus of --total-docs documents, rank r owns the contiguous range
+    [r*T/N, (r+1)*T/N) (index.json insertion order, encrypted_storage.py:136-141)."""
     from fheicp.datagen import corpus
-    # global corpus of world*docs documents; this rank owns a contiguous range
+    if args.workload == "c4":
+        q, docs = corpus(args.dim, args.total_docs, seed=args.seed + 100, query_seed=args.seed + 99)
+        lo, hi = rank * args.total_docs // world, (rank + 1) * args.total_docs // world
+        return q, docs[lo:hi], lo
     q, docs = corpus(args.dim, args.docs, seed=args.seed + 100 + rank, query_seed=args.seed + 99)
-    return q, docs
+    return q, docs, rank * args.docs
 
 
 def config_tag(args) -> str:
     """Which BASELINE.json config this run is (configs[1] is the metric's)."""
+    if args.workload == "c4":
+        return " (BASELINE configs[3])" if (args.total_docs, args.dim, args.n_bits) == (100_000, 16, 6) \
+            else " (custom)"
     known = {(1024, 16, 6): "configs[1]", (10000, 32, 8): "configs[2] (one GPU)",
              (12500, 16, 6): "configs[3], one GPU's share of 100k docs", (1000, 768, 8): "configs[4]"}
     tag = known.get((args.docs, args.dim, args.n_bits))
@@ -216,6 +233,8 @@ def roofline(p, brs) -> dict:
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
+    if args.workload == "auto":
+        args.workload = "c4" if world > 1 else "c2"
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     from fheicp import _lib
@@ -234,11 +253,10 @@ def main():
     from fheicp.search import sharded_topk
     T = threshold_int(model.qparams, args.min_similarity)
 
-    q_np, docs_np = shard(args, rank)
+    q_np, docs_np, base_idx = shard(args, rank, world)
     q_dev = torch.from_numpy(q_np).to(dev)
     d_dev = torch.from_numpy(docs_np).to(dev)
     B = docs_np.shape[0]
-    base_idx = rank * B
 
     def step():
         qx = model.quantize_dev(d_dev, q_dev)
@@ -271,11 +289,25 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    compares = world * B * args.steps
+    compares = (args.total_docs if args.workload == "c4" else world * B) * args.steps
     value = compares / elapsed
     ms_step = elapsed / args.steps * 1e3
 
     roof = roofline(p, br)
+    # every rank checks its own shard against the clear restatement of the
+    # reference path; the flags meet in one all-reduce (MIN)
+    par = shard_parity(args, model, q_np, docs_np, acc, below, T)
+    if world > 1:
+        flags = torch.tensor([int(par["acc_bit_exact"]), int(par["threshold_bit_exact"]),
+                              int(par["quant_params_equal"]), par["compares_checked"]], dtype=torch.int64)
+        on_dev = torch.distributed.get_backend() == "nccl"
+        mins, tot = flags[:3].to(dev if on_dev else "cpu"), flags[3:].to(dev if on_dev else "cpu")
+        torch.distributed.all_reduce(mins, op=torch.distributed.ReduceOp.MIN)
+        torch.distributed.all_reduce(tot, op=torch.distributed.ReduceOp.SUM)
+        mins, tot = mins.cpu().tolist(), int(tot.item())
+        par = {"compares_checked": tot, "ranks": world, "acc_bit_exact": bool(mins[0]),
+               "threshold_bit_exact": bool(mins[1]), "quant_params_equal": bool(mins[2])}
+        allgather_ms = time_allgather(args.top_k, dev, on_dev)
 
     out = {
         "metric": METRIC,
@@ -286,15 +318,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.workload == "c4" else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
         "config": {
-            "workload": f"batch compare 1 query x {B} encrypted docs per GPU, {args.dim}-dim, n_bits={args.n_bits}"
+            "workload": (f"search 1 query over {args.total_docs} encrypted docs sharded over {world} GPU(s)"
+                         if args.workload == "c4" else f"batch compare 1 query x {B} encrypted docs per GPU")
+                        + f", {args.dim}-dim, n_bits={args.n_bits}"
                         f"{config_tag(args)} + encrypted threshold (min_similarity {args.min_similarity}) "
                         f"+ top-{args.top_k}" + (" + RCCL top-k all-gather" if world > 1 else ""),
-            "docs_per_gpu": B, "dim": args.dim, "n_bits": args.n_bits, "msg_bits_P": P,
+            "docs_per_gpu": B, "total_docs": args.total_docs if args.workload == "c4" else world * B,
+            "dim": args.dim, "n_bits": args.n_bits, "msg_bits_P": P,
             "pbs_per_compare": n_pbs, "keyswitch_per_compare": n_pbs,
             "params": p.as_dict(), "parallelism": f"shard{world}",
         },
@@ -303,10 +338,13 @@ def main():
         "keyswitch_ms_total": round(ks["total_ms"], 3),
     }
 
+    out["parity"] = par
+    if world > 1:
+        out["allgather_ms"] = round(allgather_ms, 4)
     if rank == 0:
         out["topk_check"] = topk_check(args, model, world, oa, oi)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"], out["parity"] = cpu_leg(args, model, q_np, docs_np, acc, below, T)
+        out["cpu_baseline"] = cpu_leg(args, model, q_np, docs_np, par)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -321,7 +359,7 @@ def topk_check(args, model, world, oa, oi):
     sort by score desc, global document index breaking ties)."""
     scores = []
     for r in range(world):
-        q, docs = shard(args, r)
+        q, docs, _ = shard(args, r, world)
         scores.append(model.predict_clear(q[None, :] * docs))
     sc = np.concatenate(scores)
     keep = [(i, float(sc[i])) for i in range(len(sc)) if sc[i] >= args.min_similarity]
@@ -344,24 +382,52 @@ def cpu_sample(args, p) -> int:
     return int(max(8, min(32, round(32 * 5.6 / max(plan_cost(p), 1e-9)))))
 
 
-def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
-    """The oracle, timed on the host cores (bounded sample), and the parity
-    check of the last timed step against the clear restatement."""
+def shard_parity(args, model, q_np, docs_np, acc_dev, below_dev, T) -> dict:
+    """The last timed step's accumulators and threshold bits of this rank's
+    shard against the clear restatement of the reference path (the oracle's
+    fit + quantize + accumulate, fhe_similarity.py:88-94, :167;
+    batch_operations.py:226, :278)."""
+    from oracle import quant_ref as Q
+    X, y = __import__("fheicp.datagen", fromlist=["x"]).training_pairs(args.dim, 1000, seed=args.seed + 1)
+    oq = Q.fit_quantized_linear(X, y, args.n_bits)
+    acc_ref = Q.accumulate(oq, Q.quantize_input(oq, Q.pair_features(q_np, docs_np)))
+    scores_ref = Q.dequantize(oq, acc_ref)
+    return {
+        "compares_checked": int(len(acc_ref)),
+        "acc_bit_exact": bool(np.array_equal(acc_dev.cpu().numpy(), acc_ref)),
+        "threshold_bit_exact": bool(np.array_equal(below_dev.cpu().numpy(),
+                                                   (scores_ref < args.min_similarity).astype(np.int64))),
+        "quant_params_equal": oq.to_json() == model.qparams.to_dict(),
+    }
+
+
+def time_allgather(k, dev, on_dev, iters=20) -> float:
+    """Mean time of the search's one exchange step (the all-gather of k
+    (acc, index) pairs per rank, fheicp.search.sharded_topk), after the timed
+    region so it does not perturb it."""
+    a = torch.zeros(k, dtype=torch.int64, device=dev if on_dev else "cpu")
+    world = torch.distributed.get_world_size()
+    outs = [torch.empty_like(a) for _ in range(world)]
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        torch.distributed.all_gather(outs, a)
+        torch.distributed.all_gather(outs, a)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
+
+
+def cpu_leg(args, model, q_np, docs_np, parity):
+    """The oracle, timed on the host cores (bounded sample); adds its own
+    agreement with the clear restatement to `parity`."""
     from oracle import quant_ref as Q
     from oracle import tfhe_ref as R
     X, y = __import__("fheicp.datagen", fromlist=["x"]).training_pairs(args.dim, 1000, seed=args.seed + 1)
     oq = Q.fit_quantized_linear(X, y, args.n_bits)
     Xp = Q.pair_features(q_np, docs_np)
     acc_ref = Q.accumulate(oq, Q.quantize_input(oq, Xp))
-    acc = acc_dev.cpu().numpy()
-    below = below_dev.cpu().numpy()
-    scores_ref = Q.dequantize(oq, acc_ref)
-    parity = {
-        "compares_checked": int(len(acc)),
-        "acc_bit_exact": bool(np.array_equal(acc, acc_ref)),
-        "threshold_bit_exact": bool(np.array_equal(below, (scores_ref < args.min_similarity).astype(np.int64))),
-        "quant_params_equal": oq.to_json() == model.qparams.to_dict(),
-    }
+    T = Q.threshold_int(oq, args.min_similarity, *Q.acc_bounds(oq))
     # Oracle TFHE on C compares, the whole encrypted path: encrypt + linear +
     # decrypt + the digit sign extraction (all its KS + PBS) + decrypt.
     p = model.engine.params.as_dict()
@@ -396,7 +462,7 @@ def cpu_leg(args, model, q_np, docs_np, acc_dev, below_dev, T):
         Q.predict(oq, Xp)
     t_clear = (time.perf_counter() - t0) / reps
     base["clear_path_compares_per_s"] = round(len(Xp) / t_clear, 1)
-    return base, parity
+    return base
 
 
 def corpus_main(args, world, rank, local, dev):
@@ -416,9 +482,8 @@ def corpus_main(args, world, rank, local, dev):
     cq = CorpusQuant.calibrate(model.qparams, np.concatenate([e1, e2]))
     c = EncryptedCorpus(cq).compile(key_seed=args.seed, device=local, noise_seed=args.seed + 7)
     eng = c.engine
-    q_np, docs_np = shard(args, rank)
+    q_np, docs_np, base_idx = shard(args, rank, world)
     B = docs_np.shape[0]
-    base_idx = rank * B
     ids = (np.arange(B, dtype=np.uint64) + np.uint64(base_idx)) * np.uint64(args.dim)
     bodies, ids = c.encrypt_docs(docs_np, ids)
     bd = torch.from_numpy(bodies.view(np.int64)).to(dev)
@@ -476,7 +541,7 @@ def corpus_main(args, world, rank, local, dev):
         from oracle import quant_ref as Q
         X, y = __import__("fheicp.datagen", fromlist=["x"]).training_pairs(args.dim, 1000, seed=args.seed + 1)
         oq = Q.fit_quantized_linear(X, y, args.n_bits)
-        all_docs = np.concatenate([shard(args, r)[1] for r in range(world)])
+        all_docs = np.concatenate([shard(args, r, world)[1] for r in range(world)])
         want = Q.corpus_search(oq, cq.s_e, cq.n_e, q_np, all_docs, args.top_k, args.min_similarity)
         s = np.float64(cq.out_scale)
         got = [(int(i), float(s * np.float64(a))) for a, i in zip(oa.cpu().tolist(), oi.cpu().tolist()) if i >= 0]

@@ -95,6 +95,17 @@ class BatchConfig:
             raise ValueError("input_dim must be >= 1 and n_bits in [2, 16]")
 
 
+def _world():
+    """(world size, rank) of the torch.distributed group, (1, 0) without one."""
+    try:
+        import torch
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            return torch.distributed.get_world_size(), torch.distributed.get_rank()
+    except ImportError:  # pragma: no cover - torch is a hard dependency of the GPU path
+        pass
+    return 1, 0
+
+
 class BatchProcessor:
     def __init__(self, embedder=None, reducer=None, key_manager=None,
                  storage: Optional[EncryptedDocumentStore] = None, config: Optional[BatchConfig] = None,
@@ -351,7 +362,10 @@ class BatchProcessor:
         if k == 0:
             return []
         if self.config.fhe != "execute":
-            hits = self._search_clear(m, query, E, min_similarity)
+            if _world()[0] > 1:
+                hits = self._search_clear_sharded(m, query, E, k, min_similarity)
+            else:
+                hits = self._search_clear(m, query, E, min_similarity)
         else:
             hits = self._search_gpu(m, query, E, k, min_similarity)
         out = [(ids[i], s) for i, s in hits]
@@ -405,6 +419,25 @@ class BatchProcessor:
         s = np.float64(c.cq.out_scale)
         hits = [(ids[int(i)], float(s * np.float64(a))) for a, i in zip(oa, oi) if i >= 0]
         return hits[:top_k]
+
+    @staticmethod
+    def _search_clear_sharded(m, query, E, k, t):
+        """The clear search (fhe != "execute") under torch.distributed: each
+        rank scores its contiguous document range, keeps its top-k by (acc
+        desc, index asc), and the ranks meet in the same single all-gather
+        as the encrypted search (fheicp.search.sharded_topk)."""
+        import torch
+        from fheicp.model import threshold_int
+        from fheicp.search import host_topk, sharded_topk
+        fm = m.model._fitted()
+        world, rank = _world()
+        n = E.shape[0]
+        lo, hi = rank * n // world, (rank + 1) * n // world
+        acc = fm.clear_acc(query[None, :] * E[lo:hi]) if hi > lo else np.zeros(0, np.int64)
+        below = (acc < threshold_int(fm.qparams, t)).astype(np.int64)
+        oa, oi = sharded_topk(torch.from_numpy(acc), torch.from_numpy(below), k, lo, host_topk, world)
+        s = np.float64(fm.qparams.out_scale)
+        return [(int(i), float(s * np.float64(a))) for a, i in zip(oa.tolist(), oi.tolist()) if i >= 0]
 
     @staticmethod
     def _search_clear(m, query, E, t):

@@ -131,16 +131,18 @@ class FHESimilarityModel:
             m.model = LinearRegression.from_quant_params(QuantParams.from_dict(qd), device=device)
         return m
 
-    def save_compiled(self, path: str):
-        """Quantisation parameters AND keys (secret keys included) -> npz."""
+    def save_compiled(self, path: str, password: Optional[str] = None):
+        """Quantisation parameters AND keys -> npz (mode 0600); the secret keys
+        are Fernet-wrapped under password= or $FHE_MASTER_PASSWORD (fheicp.persist)."""
         if not self.compiled:
             raise RuntimeError("Model not compiled. Call compile() first.")
         fm = self.model._fitted()
-        persist.save_model(path, fm.qparams, fm.scheme, fm.engine.export_keys())
+        persist.save_model(path, fm.qparams, fm.scheme, fm.engine.export_keys(), password=password)
 
     @classmethod
-    def load_compiled(cls, path: str, similarity_type: str = "cosine", device: int = 0) -> "FHESimilarityModel":
-        qp, _, keys = persist.load_model(path)
+    def load_compiled(cls, path: str, similarity_type: str = "cosine", device: int = 0,
+                      password: Optional[str] = None) -> "FHESimilarityModel":
+        qp, _, keys = persist.load_model(path, password=password)
         m = cls(input_dim=len(qp.coef), n_bits=qp.n_bits, similarity_type=similarity_type, device=device)
         m.model = LinearRegression.from_quant_params(qp, device=device)
         if keys is not None:

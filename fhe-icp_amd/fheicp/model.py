@@ -199,10 +199,14 @@ class FheLinearModel:
         b = below.cpu().numpy() if threshold is not None else np.zeros(len(scores), np.int64)
         return scores, b
 
-    def predict_clear(self, X) -> np.ndarray:
-        """Concrete's fhe="disable" path: quantized integer inference in the clear (host)."""
+    def clear_acc(self, X) -> np.ndarray:
+        """Quantized integer accumulators in the clear (host): Concrete's
+        _inference on quantize(X), q_x @ q_w - zp * sum(q_w) + q_b."""
         X = np.atleast_2d(np.asarray(X))
         qp = self.qparams
         q = np.clip(np.rint(X.astype(np.float64) / qp.s_x + qp.zp_x), qp.qmin, qp.qmax).astype(np.int64)
-        acc = q @ np.asarray(qp.q_w, dtype=np.int64) + np.int64(qp.cst)
-        return np.float64(qp.out_scale) * acc.astype(np.float64)
+        return q @ np.asarray(qp.q_w, dtype=np.int64) + np.int64(qp.cst)
+
+    def predict_clear(self, X) -> np.ndarray:
+        """Concrete's fhe="disable" path: quantized integer inference in the clear (host)."""
+        return np.float64(self.qparams.out_scale) * self.clear_acc(X).astype(np.float64)

@@ -12,6 +12,7 @@ rank-ordered concatenation is exactly (acc desc, global index asc).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 
@@ -36,3 +37,17 @@ def sharded_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx
     ma, pos = topk_fn(cat_a, (cat_i < 0).to(torch.int64), k, 0)
     mi = torch.where(pos >= 0, cat_i[pos.clamp(min=0)], pos)
     return ma, mi
+
+
+def host_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx: int):
+    """Host (numpy) twin of fhe_topk for the clear search modes: entries with
+    below == 0 ordered by (acc desc, index asc); indices are base_idx +
+    position; missing slots acc = INT64_MIN, idx = -1."""
+    a = acc.cpu().numpy().astype(np.int64)
+    keep = np.arange(a.size) if below is None else np.flatnonzero(below.cpu().numpy() == 0)
+    order = keep[np.lexsort((keep, -a[keep]))][:k]
+    oa = np.full(k, np.iinfo(np.int64).min, dtype=np.int64)
+    oi = np.full(k, -1, dtype=np.int64)
+    oa[:order.size] = a[order]
+    oi[:order.size] = order + base_idx
+    return torch.from_numpy(oa), torch.from_numpy(oi)

@@ -109,13 +109,48 @@ def test_persist_roundtrip(tmp_path):
     keys = {k: np.arange(5, dtype=np.uint64) * (i + 3) for i, k in enumerate(persist.KEY_NAMES)}
     keys["bsk"][0] = np.uint64(2 ** 64 - 1)
     path = str(tmp_path / "m.npz")
-    persist.save_model(path, qp, params_for_bits(qp.msg_bits()), keys)
+    persist.save_model(path, qp, params_for_bits(qp.msg_bits()), keys, allow_plaintext_secrets=True)
     qp2, sch, k2 = persist.load_model(path)
     assert qp2.to_dict() == qp.to_dict() and sch == params_for_bits(qp.msg_bits())
     for k in persist.KEY_NAMES:
         np.testing.assert_array_equal(k2[k], keys[k])
     persist.save_model(path, qp, sch)
     assert persist.load_model(path)[2] is None
+
+
+def test_persist_wraps_secret_keys(tmp_path, monkeypatch):
+    """Secret keys are Fernet-wrapped (PBKDF2 of the password, as the
+    reference's key manager) and the file is mode 0600; no password -> refused
+    unless explicitly opted out; a wrong password -> ValueError."""
+    import os
+    import stat
+    from fheicp import persist
+    from fheicp.params import params_for_bits
+    from fheicp.sklearn import LinearRegression
+    monkeypatch.delenv("FHE_MASTER_PASSWORD", raising=False)
+    X, y = _data(16)
+    qp = LinearRegression(n_bits=6).fit(X, y).quant_params
+    rng = np.random.default_rng(3)
+    keys = {"s_small": rng.integers(0, 2, 887).astype(np.uint64), "s_big": rng.integers(0, 2, 2048).astype(np.uint64),
+            "bsk": rng.integers(0, 2 ** 63, 64, dtype=np.uint64), "ksk": rng.integers(0, 2 ** 63, 64, dtype=np.uint64)}
+    sch = params_for_bits(qp.msg_bits())
+    path = str(tmp_path / "m.npz")
+    with pytest.raises(ValueError):
+        persist.save_model(path, qp, sch, keys)
+    persist.save_model(path, qp, sch, keys, password="pw")
+    assert stat.S_IMODE(os.stat(path).st_mode) == 0o600
+    raw = open(path, "rb").read()
+    for k in ("s_small", "s_big"):
+        assert keys[k].tobytes() not in raw
+        assert np.packbits(keys[k].astype(np.uint8)).tobytes() not in raw
+    with pytest.raises(ValueError):
+        persist.load_model(path)                      # no password
+    with pytest.raises(ValueError):
+        persist.load_model(path, password="nope")
+    monkeypatch.setenv("FHE_MASTER_PASSWORD", "pw")
+    _, _, k2 = persist.load_model(path)
+    for k in persist.KEY_NAMES:
+        np.testing.assert_array_equal(k2[k], keys[k])
 
 
 # ------------------------------------------------------- encrypted_storage --

@@ -105,8 +105,9 @@ def test_corpus_compare_clipped_and_extreme_queries(corpus16):
         np.testing.assert_array_equal(below.cpu().numpy(), (scores < 0.0).astype(np.int64))
 
 
-def test_batch_processor_ciphertext_store(tmp_path, need_gpu):
+def test_batch_processor_ciphertext_store(tmp_path, need_gpu, monkeypatch):
     from batch_operations import BatchConfig, BatchProcessor
+    monkeypatch.setenv("FHE_MASTER_PASSWORD", "corpus-pw")   # wraps the corpus file's secret keys
     from encrypted_storage import CIPHERTEXT_VERSION, EncryptedDocumentStore
     cfg = BatchConfig(input_dim=16, n_bits=6, seed=3, key_seed=8, store_ciphertexts=True,
                       corpus_path=str(tmp_path / "corpus.npz"), batch_size=100, key_manager_default=False)

@@ -39,8 +39,9 @@ def test_estimator_threshold_bit(fitted):
         np.testing.assert_array_equal(keep, clear >= t)
 
 
-def test_similarity_model_encrypted_and_key_persistence(need_gpu, tmp_path):
+def test_similarity_model_encrypted_and_key_persistence(need_gpu, tmp_path, monkeypatch):
     from fhe_similarity import FHESimilarityModel
+    monkeypatch.setenv("FHE_MASTER_PASSWORD", "persist-pw")   # wraps the secret keys (fheicp.persist)
     m = FHESimilarityModel(input_dim=16, n_bits=6, seed=12)
     X, _ = m.train()
     m.compile(X[:10], key_seed=5)

@@ -158,3 +158,59 @@ def test_sharded_topk_equals_global(world, k):
     ga, gi = cpu_topk(torch.tensor(acc_all), torch.tensor(below_all), k, 0)
     for _, oa, oi in res:
         assert oa == ga.tolist() and oi == gi.tolist()
+
+
+def _proc_worker(rank, world, port, store_dir, query, cases, q):
+    import sys as _s
+    from pathlib import Path as _P
+    root = _P(__file__).resolve().parents[1]
+    for p in (str(root / "fhe-icp_amd"), str(root)):
+        if p not in _s.path:
+            _s.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from batch_operations import BatchConfig, BatchProcessor
+    from encrypted_storage import EncryptedDocumentStore
+    cfg = BatchConfig(fhe="disable", input_dim=16, n_bits=6, seed=21, show_progress=False,
+                      key_manager_default=False)
+    p = BatchProcessor(storage=EncryptedDocumentStore(store_dir), config=cfg)
+    res = [p.search_vector(np.asarray(query), k, t) for k, t in cases]
+    q.put((rank, res, p.fhe_model.model.quant_params.to_dict()))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_processor_sharded_search_gloo(tmp_path, monkeypatch, world):
+    """BatchProcessor.search_vector under torch.distributed (gloo, 2 and 3
+    ranks, a ragged 301-document store with duplicated documents): each rank
+    scores its contiguous range, one all-gather merges the top-k, and every
+    rank returns batch_operations.py:268-284's result (float >=, stable sort
+    desc, slice), restated by the oracle over the whole store."""
+    from encrypted_storage import EncryptedDocument, EncryptedDocumentStore
+    from oracle import quant_ref as Q
+    monkeypatch.setattr(EncryptedDocument, "allowed_dims", (16, 128, 256))
+    qv, docs = Q.make_corpus(16, 301, seed=77)
+    docs[5] = docs[200]
+    docs[150] = docs[151]                       # ties across the rank boundary
+    store = EncryptedDocumentStore(str(tmp_path))
+    ids = [f"d{i:03d}" for i in range(len(docs))]
+    store.save_many([EncryptedDocument(doc_id=ids[i], content_hash=f"{i:064x}", timestamp="2025-01-01T00:00:00",
+                                       encrypted_embedding=docs[i], metadata={}) for i in range(len(docs))])
+    cases = [(10, 0.5), (400, -100.0), (3, 100.0), (1, 0.0)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_proc_worker, args=(r, world, port, str(tmp_path), qv.tolist(), cases, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    qp = Q.QuantizedLinearParams.from_json(res[0][2])
+    for _, got, qd in res:
+        assert qd == res[0][2]
+        for (k, t), g in zip(cases, got):
+            want = [(ids[i], s) for i, s in Q.search(qp, qv, docs, k, t)]
+            assert g == want, (k, t)

@@ -12,7 +12,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 
   -d "$OUT/f64" -o pmc --output-format csv -- python3 $CMD > "$OUT/f64.log" 2>&1 || exit 1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc --output-format csv -- python3 $CMD > "$OUT/fetch.log" 2>&1 || exit 1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o pmc --output-format csv -- python3 $CMD > "$OUT/write.log" 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $CMD > "$OUT/trace.log" 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/trace.log" 2>&1 || exit 1
 python3 tools/br_pmc.py --lib fhe-icp_amd/fheicp/libfheicp.so --cts "${CTS:-1024}" --f64 "$(csvof "$OUT/f64")" \
   --fetch "$(csvof "$OUT/fetch")" --write "$(csvof "$OUT/write")" \
   --trace "$(ls "$OUT"/trace/*kernel_trace.csv "$OUT"/trace/*/*kernel_trace.csv 2>/dev/null | head -n1)" \

@@ -1,11 +1,15 @@
 #!/bin/bash
-# Round-2 GPU pass: the whole -m gpu suite (incl. the per-config and noise
-# tests), smoke, the PMC passes of the headline bench, the bench itself.
+# Round-2 GPU pass: the whole -m gpu suite, smoke, the PMC passes + kernel
+# trace of the headline bench, the bench itself, the other configs and a
+# 2-rank gloo rehearsal of the N > 1 (C4, 100k docs) path on one GPU.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"; cd "$R"
-timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -s > "$OUT/r02_tests.log" 2>&1 || exit 1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/r02_smoke.log" 2>&1 || exit 1
-bash tools/pmc_bench.sh || exit 1
+step() { echo "== $1 $(date +%T)" >> "$OUT/steps.log"; }
+step tests; timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -s > "$OUT/r02_tests.log" 2>&1 || exit 1
+step smoke; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/r02_smoke.log" 2>&1 || exit 1
+step pmc; bash tools/pmc_bench.sh || exit 1
 cp "$OUT/pmc_bench/br_pmc.json" profiles/br_pmc.json
-timeout -k 10 600 python bench.py > "$OUT/r02_bench.json" 2> "$OUT/r02_bench.err" || exit 1
-bash tools/bench_configs.sh || exit 1
+step bench; timeout -k 10 600 python bench.py > "$OUT/r02_bench.json" 2> "$OUT/r02_bench.err" || exit 1
+step configs; bash tools/bench_configs.sh || exit 1
+step n2; FHEICP_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 > "$OUT/r02_n2.json" 2> "$OUT/r02_n2.err" || exit 1
+step done
