@@ -58,29 +58,34 @@ __device__ __forceinline__ u64 block_sum_u64(u64 v, u64* red) {
 
 
 // Test vector of a bootstrap, TV_j for j in [0, N), extended negacyclically:
-//  - staircase (lut == nullptr): TV_j = base + (j >> shift) * step (step 0:
-//    a constant);
-//  - table (fhe_pbs_table_batch): 2^lut_bits boxes of 2^lut_log_box
-//    coefficients centred on the messages m * N / 2^lut_bits, TV_j =
-//    lut[m] * delta; the half box below 0 is the negacyclic image of the top
-//    half box, so a message-0 phase with negative noise still reads lut[0].
+// a staircase TV_j = base + (j >> shift) * step (step 0: a constant).
 struct BrTv {
   u64 base, step;
   int shift;
-  int lut_log_box = 0;
-  int lut_count = 0;
-  const int64_t* lut = nullptr;  // device, lut_count entries
-  u64 delta = 0;
+};
+// Table form (fhe_pbs_table_batch): 2^lut_bits boxes of 2^lut_log_box
+// coefficients centred on the messages m * N / 2^lut_bits, TV_j = lut[m] *
+// delta; the half box below 0 is the negacyclic image of the top half box, so
+// a message-0 phase with negative noise still reads lut[0]. Only the v1/v2
+// kernels take it: the hot v4 kernels keep the three-word argument (the
+// wider one measured 2-3% slower at (23,1), tools/ab_lib2.sh).
+struct BrTvLut {
+  u64 base, step;
+  int shift;
+  int lut_log_box;
+  int lut_count;
+  const int64_t* lut;  // device, lut_count entries
+  u64 delta;
 };
 __device__ __forceinline__ u64 tv_rot(const BrTv& tv, uint32_t idx, int N) {
   const uint32_t j = idx & (uint32_t)(N - 1);
-  u64 v;
-  if (tv.lut) {
-    const uint32_t box = (j + (1u << (tv.lut_log_box - 1))) >> tv.lut_log_box;
-    v = box < (uint32_t)tv.lut_count ? (u64)tv.lut[box] * tv.delta : (u64)0 - (u64)tv.lut[0] * tv.delta;
-  } else {
-    v = tv.base + (u64)(j >> tv.shift) * tv.step;
-  }
+  const u64 v = tv.base + (u64)(j >> tv.shift) * tv.step;
+  return idx < (uint32_t)N ? v : (u64)0 - v;
+}
+__device__ __forceinline__ u64 tv_rot(const BrTvLut& tv, uint32_t idx, int N) {
+  const uint32_t j = idx & (uint32_t)(N - 1);
+  const uint32_t box = (j + (1u << (tv.lut_log_box - 1))) >> tv.lut_log_box;
+  const u64 v = box < (uint32_t)tv.lut_count ? (u64)tv.lut[box] * tv.delta : (u64)0 - (u64)tv.lut[0] * tv.delta;
   return idx < (uint32_t)N ? v : (u64)0 - v;
 }
 // Output of one extracted LWE word x (word `pos` of ciphertext c):
@@ -88,7 +93,8 @@ __device__ __forceinline__ u64 tv_rot(const BrTv& tv, uint32_t idx, int N) {
 //   mode 1: sign-bit round: bit = trivial(tv.base) - x; ct_v -= bit;
 //           refreshed += bit (if given); sign = bit (if given)
 //   mode 2: digit round: ct_v -= x; refreshed += x (if given)
-__device__ __forceinline__ void br_emit(int mode, u64 x, bool body, const BrTv& tv, size_t pos, u64* out, u64* ct_v,
+template <class TV>
+__device__ __forceinline__ void br_emit(int mode, u64 x, bool body, const TV& tv, size_t pos, u64* out, u64* ct_v,
                                         u64* refreshed, u64* sign) {
   if (mode == 0) {
     out[pos] = x;

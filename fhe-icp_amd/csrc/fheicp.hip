@@ -42,6 +42,7 @@ struct fhe_ctx {
   bool keys = false;
   u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
   c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr, *tw4 = nullptr;
+  c64* bsk_fft_v2 = nullptr;  // v2-layout copy of the main BSK for the table bootstrap (made on first use)
   // bootstrapping keys of the fast gadgets (p.pbs_fast_*, p.pbs_fast2_*),
   // coefficient domain and FFT form
   u64* bskf[2] = {nullptr, nullptr};
@@ -344,7 +345,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     for (void* ptr : {(void*)ctx->s_small, (void*)ctx->s_big, (void*)ctx->bsk, (void*)ctx->ksk,
                       (void*)ctx->ksk_colsum, (void*)ctx->bsk_fft, (void*)ctx->tw, (void*)ctx->twist, ctx->ws,
                       (void*)ctx->bskf[0], (void*)ctx->bskf[1], (void*)ctx->bskf_fft[0], (void*)ctx->bskf_fft[1],
-                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4})
+                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2})
       (void)hipFree(ptr);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_brf[0]);
@@ -450,6 +451,11 @@ static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* b
 }
 static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
   const fhe_params& p = ctx->p;
+  if (ctx->bsk_fft_v2) {  // the table bootstrap's copy of the old key
+    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, hipFree(ctx->bsk_fft_v2));
+    ctx->bsk_fft_v2 = nullptr;
+  }
   hipLaunchKernelGGL(k_ksk_colsum, dim3((p.n + 1 + 255) / 256), dim3(256), 0, st, ctx->ksk, p.k * p.N * p.ks_level,
                      p.n, ctx->ksk_colsum);
   if (ctx->ks_variant == 2) {
@@ -799,13 +805,13 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   do {                                                                                                        \
     hipLaunchKernelGGL((k_blind_rotate<LOGM, K>), g, b, 0, st, d_small, p.n, p.pbs_level, p.pbs_base_log,    \
                        bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign);                  \
-    name = "k_blind_rotate<" #LOGM ", " #K ">";                                                               \
+    name = "k_blind_rotate<" #LOGM ", " #K ", BrTv>";                                                         \
   } while (0)
 #define BRV(V, K, W)                                                                                          \
   do {                                                                                                        \
     hipLaunchKernelGGL((k_blind_rotate_mw<V, K, W>), g, dim3(V::NT), 0, st, d_small, p.n, p.pbs_level,        \
                        p.pbs_base_log, bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign);   \
-    name = "k_blind_rotate_mw<fhei::" #V ", " #K ", " #W ">";                                                 \
+    name = "k_blind_rotate_mw<fhei::" #V ", " #K ", " #W ", BrTv>";                                           \
   } while (0)
 #define BR4F(L, A32, D, GG, FLAGS)                                                                            \
   do {                                                                                                        \
@@ -879,6 +885,55 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
                    (hipStream_t)stream);
 }
 
+// The table bootstrap runs on the v2 kernel at N = 1024 (v1 otherwise),
+// instantiated for the wide test-vector argument (BrTvLut); it is not on the
+// compare's hot path, which keeps the v4 kernels' three-word one.
+static int launch_br_table(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const BrTvLut& tv, uint64_t* out,
+                           hipStream_t st) {
+  const fhe_params& p = ctx->p;
+  hipEvent_t e1;
+  prof_begin(ctx, ctx->prof_br, st, &e1);
+  const char* name = nullptr;
+  const dim3 g((unsigned)count), b(64);
+#define BRT(LOGM, K)                                                                                          \
+  do {                                                                                                        \
+    hipLaunchKernelGGL((k_blind_rotate<LOGM, K, BrTvLut>), g, b, 0, st, d_small, p.n, p.pbs_level,            \
+                       p.pbs_base_log, ctx->bsk_fft, ctx->tw, ctx->twist, tv, 0, out, nullptr, nullptr, nullptr); \
+    name = "k_blind_rotate<" #LOGM ", " #K ", BrTvLut>";                                                      \
+  } while (0)
+  if (p.N == 1024 && variant_for(ctx, p) == 4) {
+    // the BSK is in the v4 FFT layout: build a v2-layout copy once
+    if (!ctx->bsk_fft_v2) {
+      HIPCHK(ctx, hipMalloc(&ctx->bsk_fft_v2, sizeof(c64) * fhe_bsk_words(&p) / 2));
+      const int npoly = (int)(fhe_bsk_words(&p) / p.N);
+      hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist,
+                         ctx->bsk_fft_v2);
+    }
+  }
+  const c64* bsk = (p.N == 1024 && ctx->bsk_fft_v2) ? ctx->bsk_fft_v2 : ctx->bsk_fft;
+  if (p.N == 1024) {
+    if (p.k == 1) {
+      hipLaunchKernelGGL((k_blind_rotate_mw<V2, 1, 2, BrTvLut>), g, dim3(V2::NT), 0, st, d_small, p.n, p.pbs_level,
+                         p.pbs_base_log, bsk, ctx->tw, ctx->twist, tv, 0, out, nullptr, nullptr, nullptr);
+      name = "k_blind_rotate_mw<fhei::V2, 1, 2, BrTvLut>";
+    } else {
+      hipLaunchKernelGGL((k_blind_rotate_mw<V2, 2, 2, BrTvLut>), g, dim3(V2::NT), 0, st, d_small, p.n, p.pbs_level,
+                         p.pbs_base_log, bsk, ctx->tw, ctx->twist, tv, 0, out, nullptr, nullptr, nullptr);
+      name = "k_blind_rotate_mw<fhei::V2, 2, 2, BrTvLut>";
+    }
+  } else if (p.N == 256 && p.k == 1) BRT(7, 1);
+  else if (p.N == 256 && p.k == 2) BRT(7, 2);
+  else if (p.N == 512 && p.k == 1) BRT(8, 1);
+  else if (p.N == 512 && p.k == 2) BRT(8, 2);
+  else if (p.N == 2048 && p.k == 1) BRT(10, 1);
+  else return fail(ctx, FHE_E_ARG, "unsupported (N, k)");
+#undef BRT
+  ctx->prof_br.kernel = name;
+  prof_end(ctx, ctx->prof_br, st, e1, count);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
 int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const int64_t* d_lut, int32_t lut_bits,
                         uint64_t* d_out, void* stream) {
   int rc = need_keys(ctx);
@@ -887,12 +942,8 @@ int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, co
   if (count < 0 || lut_bits < 0 || lut_bits > logN - 1 || !d_lut || (count > 0 && (!d_small || !d_out)))
     return fail(ctx, FHE_E_ARG, "bad pbs-table arguments (0 <= lut_bits <= log2(N) - 1)");
   if (count == 0) return FHE_OK;
-  BrTv tv{0, 0, 0};
-  tv.lut = d_lut;
-  tv.lut_count = 1 << lut_bits;
-  tv.lut_log_box = logN - lut_bits;
-  tv.delta = 1ull << (64 - ctx->p.msg_bits);
-  return launch_br(ctx, d_small, count, tv, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+  BrTvLut tv{0, 0, 0, logN - lut_bits, 1 << lut_bits, d_lut, 1ull << (64 - ctx->p.msg_bits)};
+  return launch_br_table(ctx, d_small, count, tv, d_out, (hipStream_t)stream);
 }
 
 static int ensure_ws(fhe_ctx* ctx, size_t bytes) {

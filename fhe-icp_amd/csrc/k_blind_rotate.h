@@ -10,10 +10,10 @@
 #endif
 #include "br_v4.h"
 
-template <int LOGM, int K>
+template <int LOGM, int K, class TV = BrTv>
 __global__ void __launch_bounds__(64) k_blind_rotate(const u64* __restrict__ small, int n, int L, int beta,
                                                      const c64* __restrict__ bsk, const c64* __restrict__ tw,
-                                                     const c64* __restrict__ twist, BrTv tv, int mode,
+                                                     const c64* __restrict__ twist, TV tv, int mode,
                                                      u64* __restrict__ out, u64* __restrict__ ct_v,
                                                      u64* __restrict__ refreshed, u64* __restrict__ sign) {
   using F = WaveFFT<LOGM>;
@@ -135,10 +135,10 @@ __global__ void __launch_bounds__(V::NT) k_bsk_to_fft_mw(const u64* __restrict__
   for (int u = 0; u < S; ++u) dst[V::fslot(tid, u)] = {v[0][u].x * inv, v[0][u].y * inv};
 }
 
-template <class V, int K, int MINW>
+template <class V, int K, int MINW, class TV = BrTv>
 __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __restrict__ small, int n, int L, int beta,
                                                               const c64* __restrict__ bsk, const c64* __restrict__ tw,
-                                                              const c64* __restrict__ twist, BrTv tv, int mode,
+                                                              const c64* __restrict__ twist, TV tv, int mode,
                                                               u64* __restrict__ out, u64* __restrict__ ct_v,
                                                               u64* __restrict__ refreshed, u64* __restrict__ sign) {
   constexpr int M = V::M, N = V::N, S = V::S, NT = V::NT;

@@ -26,11 +26,11 @@ INSTANCES = {
     (15, 2): "k_blind_rotate_v4<2, true, 0, 4, false>",
     (23, 1): "k_blind_rotate_v4<1, true, 0, 4, false>",
     (12, 3): "k_blind_rotate_v4<3, false, 0, 2, false>",
-    (10, 4): "k_blind_rotate_mw<fhei::V2, 2, 2>",
-    (8, 5): "k_blind_rotate_mw<fhei::V2, 2, 2>",
-    (7, 6): "k_blind_rotate_mw<fhei::V2, 2, 2>",
-    (6, 7): "k_blind_rotate_mw<fhei::V2, 2, 2>",
-    (5, 8): "k_blind_rotate_mw<fhei::V2, 2, 2>",
+    (10, 4): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (8, 5): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (7, 6): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (6, 7): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (5, 8): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
 }
 COUNT = 4096
 TV = 1 << 61
