@@ -68,6 +68,7 @@ class BatchConfig:
     input_dim: int = field(default_factory=lambda: int(os.environ.get("FHE_ICP_DIM", "128")))
     n_bits: int = field(default_factory=lambda: int(os.environ.get("FHE_ICP_N_BITS", "8")))
     reducer_path: str = "pca_reducer_128.pkl"  # DimensionReducer.load (:63)
+    gpu_reducer: bool = False       # run a fitted PCA DimensionReducer on the GPU (fheicp.pca, §8f-4)
     key_manager_default: bool = True  # no key_manager given: FHEKeyManager() as the reference (:64)
     device: int = 0
     model_path: Optional[str] = None  # fheicp.persist file: load instead of retrain (§8f-2)
@@ -250,6 +251,9 @@ class BatchProcessor:
         if self.reducer is None:
             from dimension_reduction import DimensionReducer
             self.reducer = DimensionReducer.load(self.config.reducer_path)
+        if self.config.gpu_reducer and not hasattr(self.reducer, "transform_dev"):
+            from fheicp.pca import GpuPCA
+            self.reducer = GpuPCA.from_reducer(self.reducer, device=self.config.device)
         return self.embedder, self.reducer
 
     def _embed(self, texts: List[str]) -> np.ndarray:

@@ -1207,6 +1207,20 @@ int fhe_quantize_pairs(fhe_ctx* ctx, const void* d_query, int32_t query_is_f64, 
   return FHE_OK;
 }
 
+int fhe_pca_transform(fhe_ctx* ctx, const float* d_x, int64_t B, int32_t K, const float* d_mean,
+                      const float* d_components, int32_t D, float* d_out, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (B < 0 || K <= 0 || K > 1024 || D <= 0 || (B > 0 && (!d_x || !d_mean || !d_components || !d_out)))
+    return fail(ctx, FHE_E_ARG, "bad pca arguments (1 <= K <= 1024, D >= 1)");
+  if (B == 0) return FHE_OK;
+  if (B > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "pca batch too large: split the call");
+  hipLaunchKernelGGL(k_pca_transform, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, d_x, (int)K, d_mean,
+                     d_components, (int)D, d_out);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
 int fhe_dequantize(fhe_ctx* ctx, const int64_t* d_acc, int64_t B, double out_scale, double* d_score, void* stream) {
   int rc = need_device(ctx);
   if (rc) return rc;

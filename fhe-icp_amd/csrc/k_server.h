@@ -309,3 +309,27 @@ __global__ void __launch_bounds__(1024) k_topk(const int64_t* __restrict__ accv,
     __syncthreads();
   }
 }
+
+// PCA transform of the embedding stage (dimension_reduction.py:67-72, sklearn
+// PCA.transform without whitening): out[b][d] = sum_k (x[b][k] - mean[k]) *
+// comp[d][k], accumulated in f64 (a fixed summation order: deterministic, and
+// at least as accurate as the reference's float32 BLAS), stored as float32 as
+// the reference stores embeddings (batch_operations.py:175-178). One 256-thread
+// workgroup per row; the row (K <= 1024 floats, centred) is staged in LDS and
+// each thread owns outputs d = tid, tid + 256, ...; the components (D x K)
+// stay L2-resident across rows.
+__global__ void __launch_bounds__(256) k_pca_transform(const float* __restrict__ x, int K,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ comp, int D,
+                                                       float* __restrict__ out) {
+  __shared__ double row[1024];
+  const int64_t b = blockIdx.x;
+  for (int k = threadIdx.x; k < K; k += 256) row[k] = (double)x[(size_t)b * K + k] - (double)mean[k];
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += 256) {
+    const float* c = comp + (size_t)d * K;
+    double acc = 0.0;
+    for (int k = 0; k < K; ++k) acc = __fma_rn(row[k], (double)c[k], acc);
+    out[(size_t)b * D + d] = (float)acc;
+  }
+}

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("fhe_key_from_seed", None, [_u64, _vp]),
     ("fhe_quantize_pairs", C.c_int, [_CTXP, _vp, _i32, _vp, _i32, _i64, _i32, C.c_double, _i64, _i64, _i64, _vp, _vp]),
     ("fhe_dequantize", C.c_int, [_CTXP, _vp, _i64, C.c_double, _vp, _vp]),
+    ("fhe_pca_transform", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     ("fhe_topk", C.c_int, [_CTXP, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     ("fhe_dev_alloc", C.c_int, [_CTXP, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("fhe_dev_free", C.c_int, [_CTXP, _vp]),

@@ -249,6 +249,14 @@ void fhe_key_from_seed(uint64_t seed, uint32_t h_key_out[8]);
 int fhe_quantize_pairs(fhe_ctx* ctx, const void* d_query, int32_t query_is_f64, const void* d_docs,
                        int32_t docs_is_f64, int64_t B, int32_t D, double scale, int64_t zero_point, int64_t qmin,
                        int64_t qmax, int64_t* d_qx, void* stream);
+/* The embedding stage's PCA (dimension_reduction.py:67-72: sklearn
+ * PCA.transform, no whitening), SURVEY.md §8f-4: d_out[b][d] = sum_k
+ * (d_x[b][k] - d_mean[k]) * d_components[d][k] for B rows of K <= 1024
+ * float32 features and D components (row-major, as PCA.components_),
+ * accumulated in f64 and stored as float32 (the reference stores float32
+ * embeddings, batch_operations.py:175-178). Needs no keys. */
+int fhe_pca_transform(fhe_ctx* ctx, const float* d_x, int64_t B, int32_t K, const float* d_mean,
+                      const float* d_components, int32_t D, float* d_out, void* stream);
 /* score[b] = out_scale * (double)acc[b] (UniformQuantizer.dequant, zp 0) */
 int fhe_dequantize(fhe_ctx* ctx, const int64_t* d_acc, int64_t B, double out_scale, double* d_score, void* stream);
 
