@@ -118,13 +118,18 @@ def config_tag(args) -> str:
     return f" (BASELINE {tag})" if tag else " (custom)"
 
 
-def br_flops_per_ct(p) -> float:
+def br_flops_per_ct(p, group: int = 1) -> float:
     """Analytic f64 FLOPs of one blind rotation (radix-2 FFT count, DESIGN.md
-    §4.2); used only when no PMC measurement of this build exists."""
+    §4.2); used only when no PMC measurement of this build exists. Group 2
+    (multi-bit, §4.5): per pair of LWE coefficients the transforms of one
+    step, three subsets' products and the (psi^(a e) - 1) factors."""
     M = p.N // 2
     logm = int(np.log2(M))
     fft = 5.0 * M * logm + 6.0 * M             # radix-2 complex FFT + twist
     nf, ni = (p.k + 1) * p.pbs_level, p.k + 1
+    if group == 2:
+        per_pair = nf * fft + ni * fft + 3 * 8.0 * nf * ni * M + p.pbs_level * 3 * ni * 9.0 * M
+        return (p.n + 1) // 2 * per_pair
     pointwise = 8.0 * nf * ni * M
     return p.n * (nf * fft + ni * fft + pointwise)
 
@@ -155,22 +160,23 @@ def read_br(eng) -> dict:
     return out
 
 
-def _br_kernel(q, br, pmc) -> dict:
+def _br_kernel(q, br, pmc, group: int = 1) -> dict:
     """One blind-rotation kernel (gadget q) from its own launches: HIP-event
     time per launch; f64 FLOPs executed per launch from the PMC pass of this
     build at this batch size (else the analytic count); algorithmic HBM bytes
     (the FFT-domain BSK once + LWE I/O) and the PMC-measured HBM bytes."""
     avg_ms = br["total_ms"] / max(br["launches"], 1)
     cts_per_launch = br["items"] / max(br["launches"], 1)
-    bsk_bytes = q.n * (q.k + 1) * q.pbs_level * (q.k + 1) * (q.N // 2) * 16
+    ggsws = 3 * ((q.n + 1) // 2) if group == 2 else q.n
+    bsk_bytes = ggsws * (q.k + 1) * q.pbs_level * (q.k + 1) * (q.N // 2) * 16
     io_bytes = cts_per_launch * ((q.n + 1) * 8 + (q.k * q.N + 1) * 8 * 5)
     alg_bytes = bsk_bytes + io_bytes
     m = pmc.get(br["kernel"], {})
     measured = bool(m) and int(m.get("cts_per_launch", -1)) == int(cts_per_launch)
-    flops = float(m["f64_flops_per_launch"]) if measured else br_flops_per_ct(q) * cts_per_launch
+    flops = float(m["f64_flops_per_launch"]) if measured else br_flops_per_ct(q, group) * cts_per_launch
     secs = avg_ms * 1e-3
     return {
-        "kernel": br["kernel"], "gadget": [q.pbs_base_log, q.pbs_level],
+        "kernel": br["kernel"], "gadget": [q.pbs_base_log, q.pbs_level], "group": group,
         "avg_launch_ms": round(avg_ms, 4), "launches": br["launches"], "cts_per_launch": cts_per_launch,
         "total_ms": round(br["total_ms"], 3),
         "f64_flops_per_launch": flops, "flops_source": "pmc" if measured else "analytic",
@@ -195,13 +201,15 @@ def roofline(p, brs) -> dict:
     three kernels run; the one with the largest total time is reported, all
     are listed under `kernels`."""
     from dataclasses import replace
-    qs = {"main": p}
+    qs = {"main": (p, 1)}
     if p.pbs_fast_level:
-        qs["fast"] = replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level)
+        qs["fast"] = (replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level),
+                      2 if p.pbs_fast_group == 2 else 1)
     if p.pbs_fast2_level:
-        qs["fast2"] = replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level)
+        qs["fast2"] = (replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level),
+                       2 if p.pbs_fast2_group == 2 else 1)
     pmc = load_pmc()
-    ks = {g: _br_kernel(q, brs[g], pmc) for g, q in qs.items() if brs[g]["launches"]}
+    ks = {g: _br_kernel(q, brs[g], pmc, grp) for g, (q, grp) in qs.items() if brs[g]["launches"]}
     dom = max(ks, key=lambda g: ks[g]["total_ms"])
     k = ks[dom]
     tf = k["achieved_tflops_f64"]

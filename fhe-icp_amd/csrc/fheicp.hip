@@ -47,6 +47,13 @@ struct fhe_ctx {
   // coefficient domain and FFT form
   u64* bskf[2] = {nullptr, nullptr};
   c64* bskf_fft[2] = {nullptr, nullptr};
+  // multi-bit blind rotation of the fast gadgets with pbs_fast*_group = 2
+  // (DESIGN.md §4.5): their keys hold three GGSWs per pair of LWE
+  // coefficients (messages in mb_msg); psi^x table, x < 2N (bank-swizzled)
+  c64* psi = nullptr;
+  u64* mb_msg = nullptr;
+  int mb_dbg = 0;      // A/B builds: FHEICP_MB_DBG timing variants of the multi-bit kernel
+  int v4s = 0;         // A/B builds: FHEICP_V4S=1, key-stationary v4s for the 32-bit kernels too
   // workspace
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -116,7 +123,23 @@ static int validate(const fhe_params* p, std::string& why) {
       (p->pbs_fast2_level && !p->pbs_fast_level)) {
     why = "fast2 pbs decomposition out of range (0, 0 for none; needs a fast gadget)"; return -1;
   }
+  for (int g = 1; g <= 2; ++g) {
+    const int grp = g == 1 ? p->pbs_fast_group : p->pbs_fast2_group;
+    const int L = g == 1 ? p->pbs_fast_level : p->pbs_fast2_level;
+    const int bl = g == 1 ? p->pbs_fast_base_log : p->pbs_fast2_base_log;
+    if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group must be 0, 1 or 2"; return -1; }
+    if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 2 && L * bl <= 31)) {
+      why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 2, level * base_log <= 31";
+      return -1;
+    }
+  }
   return 0;
+}
+
+// grouping factor of gadget g's blind rotation (0: main, always 1)
+static int gadget_group(const fhe_params& p, int g) {
+  const int v = g == 1 ? p.pbs_fast_group : g == 2 ? p.pbs_fast2_group : 1;
+  return v == 2 ? 2 : 1;
 }
 
 static double tuniform_var(int b) { return (std::ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
@@ -127,15 +150,20 @@ static double tuniform_var(int b) { return (std::ldexp(1.0, 2 * b + 1) + 1.0) / 
 // arithmetic error (C_FFT = 16 bounds the 11.6-13.8 measured on every kernel
 // instance, tests/test_gpu_noise.py) + the 2^32 rounding of the 32-bit
 // accumulators (L*beta <= 31), the last two key-weighted per step.
+// The multi-bit rotation (group 2): 3x the key noise (three
+// GGSWs per pair, each times X^a - 1), the same gadget rounding total, 3x the
+// FFT error and half the 2^32 output roundings.
 constexpr double C_FFT = 16.0;
-static double pbs_var(const fhe_params& p, int beta, int L) {
+static double pbs_var(const fhe_params& p, int beta, int L, int group = 1) {
   const double s2_bsk = tuniform_var(p.glwe_noise_bits) / std::ldexp(1.0, 128);
   const double B = std::ldexp(1.0, beta);
   const double rows = (double)L * (p.k + 1) * p.N;
   const double steps = p.n * (1 + p.k * p.N / 2.0);
-  double arith = C_FFT * rows * B * B / 144.0 * std::ldexp(1.0, -106);
-  if (beta * L <= 31) arith += std::ldexp(1.0, -64) / 12.0;
-  return p.n * rows * (B * B + 2) / 12.0 * s2_bsk + steps / (12.0 * std::pow(B, 2.0 * L)) + steps * arith;
+  const double fft = C_FFT * rows * B * B / 144.0 * std::ldexp(1.0, -106);
+  const double out32 = beta * L <= 31 ? std::ldexp(1.0, -64) / 12.0 : 0.0;
+  const double km = group == 2 ? 3.0 : 1.0;
+  const double arith = group == 2 ? 3.0 * fft + 0.5 * out32 : fft + out32;
+  return km * p.n * rows * (B * B + 2) / 12.0 * s2_bsk + steps / (12.0 * std::pow(B, 2.0 * L)) + steps * arith;
 }
 static double ks_var(const fhe_params& p) {
   const double s2_ksk = tuniform_var(p.lwe_noise_bits) / std::ldexp(1.0, 128);
@@ -174,8 +202,9 @@ static double plan_worst(const fhe_params& p, int d, int j1, int j2) {
   int sh[64], ml[64];
   const int R = sign_rounds(p.msg_bits, d, sh, ml);
   const double vm = pbs_var(p, p.pbs_base_log, p.pbs_level);
-  const double vf = p.pbs_fast_level ? pbs_var(p, p.pbs_fast_base_log, p.pbs_fast_level) : vm;
-  const double vf2 = p.pbs_fast2_level ? pbs_var(p, p.pbs_fast2_base_log, p.pbs_fast2_level) : vf;
+  const double vf = p.pbs_fast_level ? pbs_var(p, p.pbs_fast_base_log, p.pbs_fast_level, gadget_group(p, 1)) : vm;
+  const double vf2 =
+      p.pbs_fast2_level ? pbs_var(p, p.pbs_fast2_base_log, p.pbs_fast2_level, gadget_group(p, 2)) : vf;
   const double fixed = ks_var(p) + ms_var(p);
   double acc = 0, worst = 1e300;
   for (int r = 0; r < R; ++r) {
@@ -271,6 +300,8 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   }
   if (const char* e = getenv("FHEICP_V4_FL")) ctx->v4_fl = atoi(e) != 0;
   if (const char* e = getenv("FHEICP_V4_A64")) ctx->v4_a64 = atoi(e) != 0;
+  if (const char* e = getenv("FHEICP_MB_DBG")) ctx->mb_dbg = atoi(e);
+  if (const char* e = getenv("FHEICP_V4S")) ctx->v4s = atoi(e);
 #endif
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
   if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
@@ -311,8 +342,16 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
           const long double ang = 2.0L * PI * (long double)(L * m) / 64.0L;
           t4[v4::NTA + (m - 1) * 8 + L] = {(double)cosl(ang), (double)sinl(ang)};
         }
+      // psi^x = exp(i pi x / N), x < 2N: the monomial factors of the multi-bit rotation
+      std::vector<c64> ps(2 * N);
+      for (int x = 0; x < 2 * N; ++x) {
+        const long double ang = PI * (long double)x / (long double)N;
+        ps[mb::psi_pos(x)] = {(double)cosl(ang), (double)sinl(ang)};  // bank-swizzled (k_blind_rotate_mb)
+      }
       if (hipMalloc(&ctx->tw4, sizeof(c64) * t4.size()) != hipSuccess ||
-          hipMemcpy(ctx->tw4, t4.data(), sizeof(c64) * t4.size(), hipMemcpyHostToDevice) != hipSuccess) {
+          hipMemcpy(ctx->tw4, t4.data(), sizeof(c64) * t4.size(), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMalloc(&ctx->psi, sizeof(c64) * ps.size()) != hipSuccess ||
+          hipMemcpy(ctx->psi, ps.data(), sizeof(c64) * ps.size(), hipMemcpyHostToDevice) != hipSuccess) {
         fhe_ctx_destroy(ctx);
         return fail(nullptr, FHE_E_DEVICE, "twiddle upload failed");
       }
@@ -345,7 +384,8 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     for (void* ptr : {(void*)ctx->s_small, (void*)ctx->s_big, (void*)ctx->bsk, (void*)ctx->ksk,
                       (void*)ctx->ksk_colsum, (void*)ctx->bsk_fft, (void*)ctx->tw, (void*)ctx->twist, ctx->ws,
                       (void*)ctx->bskf[0], (void*)ctx->bskf[1], (void*)ctx->bskf_fft[0], (void*)ctx->bskf_fft[1],
-                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2})
+                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2,
+                      (void*)ctx->psi, (void*)ctx->mb_msg})
       (void)hipFree(ptr);
     free_ev(ctx->prof_br);
     free_ev(ctx->prof_brf[0]);
@@ -393,23 +433,39 @@ static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
 // the parameters seen through fast gadget g (1: pbs_fast_*, 2: pbs_fast2_*;
 // same secret keys, other decomposition and bootstrapping key)
 static int fast_level(const fhe_params& p, int g) { return g == 1 ? p.pbs_fast_level : p.pbs_fast2_level; }
+// fast gadget g runs the multi-bit blind rotation
+static bool mb_for(const fhe_params& p, int g) { return g > 0 && fast_level(p, g) && gadget_group(p, g) == 2; }
 static fhe_params fast_params(const fhe_params& p, int g) {
   fhe_params q = p;
   q.pbs_base_log = g == 1 ? p.pbs_fast_base_log : p.pbs_fast2_base_log;
   q.pbs_level = fast_level(p, g);
   return q;
 }
-// the fast gadgets' keys under the ChaCha20 streams 9/10 and 11/12
+// GGSWs of a fast gadget's key: one per LWE coefficient, or three per pair
+static int fast_ggsws(const fhe_params& p, int g) { return mb_for(p, g) ? 3 * ((p.n + 1) / 2) : p.n; }
+static size_t fast_bsk_words(const fhe_params& p, int g) {
+  return (size_t)fast_ggsws(p, g) * (p.k + 1) * fast_level(p, g) * (p.k + 1) * p.N;
+}
+size_t fhe_fast_bsk_words(const fhe_params* p, int32_t which) {
+  if (!p || (which != 1 && which != 2) || !fast_level(*p, which)) return 0;
+  return fast_bsk_words(*p, which);
+}
+// the fast gadgets' keys under the ChaCha20 streams 9/10 and 11/12 (13/14 and
+// 15/16 for multi-bit keys, whose GGSW messages k_mb_msgs derives)
 static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
   const fhe_params& p = ctx->p;
   const size_t shm = 8 * (size_t)p.N + p.N;
   for (int g = 1; g <= 2; ++g) {
     if (!fast_level(p, g)) continue;
     const fhe_params q = fast_params(p, g);
-    hipLaunchKernelGGL(k_keygen_bsk, dim3(q.n * (q.k + 1) * q.pbs_level), dim3(256), shm, st, K, q.N, q.k,
-                       q.pbs_level, q.pbs_base_log, q.glwe_noise_bits, ctx->s_small, ctx->s_big, ctx->bskf[g - 1],
-                       (uint32_t)(g == 1 ? TAG_BSK2_MASK : TAG_BSK3_MASK),
-                       (uint32_t)(g == 1 ? TAG_BSK2_NOISE : TAG_BSK3_NOISE));
+    const bool mb = mb_for(p, g);
+    if (mb) hipLaunchKernelGGL(k_mb_msgs, dim3((q.n + 255) / 256), dim3(256), 0, st, ctx->s_small, q.n, ctx->mb_msg);
+    hipLaunchKernelGGL(k_keygen_bsk, dim3(fast_ggsws(p, g) * (q.k + 1) * q.pbs_level), dim3(256), shm, st, K, q.N,
+                       q.k, q.pbs_level, q.pbs_base_log, q.glwe_noise_bits, mb ? ctx->mb_msg : ctx->s_small,
+                       ctx->s_big, ctx->bskf[g - 1],
+                       (uint32_t)(mb ? (g == 1 ? TAG_MB2_MASK : TAG_MB3_MASK) : (g == 1 ? TAG_BSK2_MASK : TAG_BSK3_MASK)),
+                       (uint32_t)(mb ? (g == 1 ? TAG_MB2_NOISE : TAG_MB3_NOISE)
+                                     : (g == 1 ? TAG_BSK2_NOISE : TAG_BSK3_NOISE)));
   }
 }
 static int alloc_keys(fhe_ctx* ctx) {
@@ -417,8 +473,9 @@ static int alloc_keys(fhe_ctx* ctx) {
   for (int g = 1; g <= 2; ++g) {
     if (!fast_level(p, g) || ctx->bskf[g - 1]) continue;
     const fhe_params q = fast_params(p, g);
-    HIPCHK(ctx, hipMalloc(&ctx->bskf[g - 1], 8 * fhe_bsk_words(&q)));
-    HIPCHK(ctx, hipMalloc(&ctx->bskf_fft[g - 1], sizeof(c64) * fhe_bsk_words(&q) / 2));
+    HIPCHK(ctx, hipMalloc(&ctx->bskf[g - 1], 8 * fast_bsk_words(p, g)));
+    HIPCHK(ctx, hipMalloc(&ctx->bskf_fft[g - 1], sizeof(c64) * fast_bsk_words(p, g) / 2));
+    if (mb_for(p, g) && !ctx->mb_msg) HIPCHK(ctx, hipMalloc(&ctx->mb_msg, 8 * 3 * (size_t)((q.n + 1) / 2)));
   }
   if (ctx->s_small) return FHE_OK;
   HIPCHK(ctx, hipMalloc(&ctx->s_small, 8 * (size_t)p.n));
@@ -430,13 +487,14 @@ static int alloc_keys(fhe_ctx* ctx) {
   return FHE_OK;
 }
 
-static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* bsk_fft, hipStream_t st) {
-  const int npoly = (int)(fhe_bsk_words(&p) / p.N);
+static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* bsk_fft, hipStream_t st,
+                       size_t words = 0) {
+  const int npoly = (int)((words ? words : fhe_bsk_words(&p)) / p.N);
   switch (p.N) {
     case 256: hipLaunchKernelGGL(k_bsk_to_fft<7>, dim3(npoly), dim3(64), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft); break;
     case 512: hipLaunchKernelGGL(k_bsk_to_fft<8>, dim3(npoly), dim3(64), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft); break;
     case 1024:
-      if (variant_for(ctx, p) == 4)
+      if (variant_for(ctx, p) == 4 || words)
         hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, bsk, npoly, ctx->tw4,
                            bsk_fft, (v4_a32(ctx, p) ? 1.0 / 18446744073709551616.0 : 1.0) / (double)(p.N / 2));
 #ifdef FHEICP_AB
@@ -467,7 +525,9 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
   }
   bsk_to_fft(ctx, p, ctx->bsk, ctx->bsk_fft, st);
   for (int g = 1; g <= 2; ++g)
-    if (fast_level(p, g)) bsk_to_fft(ctx, fast_params(p, g), ctx->bskf[g - 1], ctx->bskf_fft[g - 1], st);
+    if (fast_level(p, g))
+      bsk_to_fft(ctx, fast_params(p, g), ctx->bskf[g - 1], ctx->bskf_fft[g - 1], st,
+                 mb_for(p, g) ? fast_bsk_words(p, g) : 0);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -526,7 +586,7 @@ int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk) {
   if (!h_bsk) return fail(ctx, FHE_E_ARG, "null buffer");
   const fhe_params q = fast_params(ctx->p, which);
   HIPCHK(ctx, hipDeviceSynchronize());
-  HIPCHK(ctx, hipMemcpy(h_bsk, ctx->bskf[which - 1], 8 * fhe_bsk_words(&q), hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemcpy(h_bsk, ctx->bskf[which - 1], 8 * fast_bsk_words(ctx->p, which), hipMemcpyDeviceToHost));
   return FHE_OK;
 }
 
@@ -765,7 +825,18 @@ static bool launch_br_ab(fhe_ctx* ctx, const fhe_params& p, const uint64_t* d_sm
       case 32: AB4D(32); case 6: AB4D(6); case 128: AB4D(128); default: AB4D(63);
     }
   }
-  if (!(ctx->v4_g == 1 || ctx->v4_fl || (a32 && ctx->v4_g == 2) || (!a32 && ctx->v4_g == 4))) return false;
+  if (ctx->v4s && a32) {  // FHEICP_V4S=1: key-stationary products for the 32-bit kernels too
+    if (p.pbs_level == 1)
+      hipLaunchKernelGGL((k_blind_rotate_v4s<1, true>), dim3((unsigned)((count + 3) / 4)), dim3(v4::nthreads(4)), 0,
+                         st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, tv, mode, out, ct_v, refreshed, sign);
+    else
+      hipLaunchKernelGGL((k_blind_rotate_v4s<2, true>), dim3((unsigned)((count + 3) / 4)), dim3(v4::nthreads(4)), 0,
+                         st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, tv, mode, out, ct_v, refreshed, sign);
+    *name = "k_blind_rotate_v4s<A32>";
+    return true;
+  }
+  // shapes other than the shipped ones; the 64-bit v4 kernels (v4s ships)
+  if (!(ctx->v4_g == 1 || ctx->v4_fl || ctx->v4_g == 2)) return false;
   const int G = ctx->v4_g;
   switch (p.pbs_level) {
     case 1:
@@ -820,10 +891,10 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
                        tv, mode, out, ct_v, refreshed, sign);                                                 \
     name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ">";                                 \
   } while (0)
-  // The shipped v4 instances: 4 ciphertexts per workgroup (3 waves per SIMD,
-  // <= 168 VGPRs) for the 32-bit-accumulator kernels; 2 for the u64 ones
-  // (208+ VGPRs; at 4 per workgroup they spill: P=21, 22.2 vs 20.9 ms per
-  // 1024 bootstraps). Other shapes are A/B builds (FHEICP_AB).
+  // The shipped N = 1024, k = 2 instances: the multi-bit kernels for fast
+  // gadgets with pbs_fast*_group = 2; v4 at 4 ciphertexts per workgroup (3
+  // waves per SIMD, <= 168 VGPRs) for the 32-bit accumulators; v4s for the
+  // 64-bit ones. Other shapes are A/B builds (FHEICP_AB).
   bool done = false;
 #ifdef FHEICP_AB
   if (p.N == 1024 && p.k == 2 && var == 4) done = launch_br_ab(ctx, p, d_small, count, tv, mode, out, ct_v, refreshed, sign,
@@ -834,13 +905,53 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   }
 #endif
   if (done) {
-  } else if (p.N == 1024 && p.k == 2 && var == 4) {
-    const bool a32 = v4_a32(ctx, p);
+  } else if (fast && mb_for(ctx->p, gad)) {
+    // multi-bit rotation, key-stationary products (k_blind_rotate_mb)
+    const dim3 gm((unsigned)((count + 3) / 4)), bm(v4::nthreads(4));
+#define MBD(L, D)                                                                                               \
+  hipLaunchKernelGGL((k_blind_rotate_mb<L, D>), gm, bm, 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, \
+                     ctx->tw4, ctx->psi, tv, mode, out, ct_v, refreshed, sign)
+#ifdef FHEICP_AB
+    if (ctx->mb_dbg) {
+      const int w = ctx->mb_dbg >> 8;
+      if (ctx->mb_dbg == 2) { if (p.pbs_level == 1) MBD(1, 2); else MBD(2, 2); }
+      else if (ctx->mb_dbg == 130) { if (p.pbs_level == 1) MBD(1, 130); else MBD(2, 130); }
+      else if (w == 0) { if (p.pbs_level == 1) MBD(1, 128); else MBD(2, 128); }
+      else if (w == 1) { if (p.pbs_level == 1) MBD(1, 128 + 256); else MBD(2, 128 + 256); }
+      else { if (p.pbs_level == 1) MBD(1, 128 + 512); else MBD(2, 128 + 512); }
+      name = "k_blind_rotate_mb<DBG>";
+    } else
+#endif
+    if (p.pbs_level == 1) {
+      MBD(1, 0);
+      name = "k_blind_rotate_mb<1, 0>";
+    } else {
+      MBD(2, 0);
+      name = "k_blind_rotate_mb<2, 0>";
+    }
+#undef MBD
+  } else if (p.N == 1024 && p.k == 2 && var == 4 && !v4_a32(ctx, p)) {
+    // 64-bit accumulators: the key-stationary v4s kernels, 4 ciphertexts per
+    // workgroup (15.9 vs 20.7 ms per 1024 at (12,3) for v4 at 2 per workgroup)
+#define BR4S(L)                                                                                               \
+  do {                                                                                                        \
+    hipLaunchKernelGGL((k_blind_rotate_v4s<L, false>), dim3((unsigned)((count + 3) / 4)), dim3(v4::nthreads(4)), \
+                       0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, tv, mode, out, ct_v,    \
+                       refreshed, sign);                                                                      \
+    name = "k_blind_rotate_v4s<" #L ", false, 0>";                                                             \
+  } while (0)
     switch (p.pbs_level) {
-      case 1: if (a32) BR4F(1, true, 0, 4, false); else BR4F(1, false, 0, 2, false); break;
-      case 2: if (a32) BR4F(2, true, 0, 4, false); else BR4F(2, false, 0, 2, false); break;
-      case 3: BR4F(3, false, 0, 2, false); break;
+      case 1: BR4S(1); break;
+      case 2: BR4S(2); break;
+      case 3: BR4S(3); break;
       default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: pbs_level > 3");
+    }
+#undef BR4S
+  } else if (p.N == 1024 && p.k == 2 && var == 4) {
+    switch (p.pbs_level) {
+      case 1: BR4F(1, true, 0, 4, false); break;
+      case 2: BR4F(2, true, 0, 4, false); break;
+      default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: 32-bit accumulators need pbs_level <= 2");
     }
   } else if (p.N == 256 && p.k == 1) BR(7, 1);
   else if (p.N == 256 && p.k == 2) BR(7, 2);
@@ -865,6 +976,18 @@ int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t
   if (count < 0 || (count > 0 && (!d_small || !d_out))) return fail(ctx, FHE_E_ARG, "bad pbs arguments");
   if (count == 0) return FHE_OK;
   return launch_br(ctx, d_small, count, BrTv{tv, 0, 0}, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int fhe_pbs_gadget_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, int32_t gadget, uint64_t tv,
+                         uint64_t* d_out, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || gadget < 0 || gadget > 2 || (count > 0 && (!d_small || !d_out)))
+    return fail(ctx, FHE_E_ARG, "bad pbs-gadget arguments");
+  if (gadget > 0 && !fast_level(ctx->p, gadget)) return fail(ctx, FHE_E_STATE, "no such fast gadget in these parameters");
+  if (count == 0) return FHE_OK;
+  return launch_br(ctx, d_small, count, BrTv{tv, 0, 0}, 0, d_out, nullptr, nullptr, nullptr, (hipStream_t)stream,
+                   gadget);
 }
 
 static int log2i(int x) {

@@ -351,7 +351,11 @@ __device__ unsigned long long g_v4_stamps[4][16];
 __device__ unsigned long long g_v4_span[2048][3];
 #define V4_STAMP(k)                                                                        \
   do {                                                                                     \
-    if constexpr ((DBG & 128) != 0) stamp_[k] = __builtin_amdgcn_s_memtime();              \
+    if constexpr ((DBG & 128) != 0) {                                                      \
+      __builtin_amdgcn_sched_barrier(0);                                                   \
+      stamp_[k] = __builtin_amdgcn_s_memtime();                                            \
+      __builtin_amdgcn_sched_barrier(0);                                                   \
+    }                                                                                      \
   } while (0)
 
 // DBG != 0 only for timing experiments (tools/prof_br.py, FHEICP_V4_DBG):
@@ -595,4 +599,411 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
   }
 }
 
-// acc_out[b] = v[b] + T
+// ---- multi-bit blind rotation (grouping factor 2) on the v4 layout ---------
+// DESIGN.md §4.5. The LWE mask coefficients go in pairs (a1, a2) with secret
+// bits (s1, s2); the key holds, per pair, GGSWs of the three indicators
+// m_S = [s1 s2 pattern = S] for S = {1}, {2}, {1,2} (k_mb_msgs). One step per
+// pair:
+//   ACC += ExtProd(ACC, sum_S (X^{a_S} - 1) GGSW(m_S)),  a_{1,2} = a1 + a2,
+// which rotates ACC by a1 s1 + a2 s2: exactly one m_S is 1 unless s1 = s2 = 0.
+// The monomials act in the FFT domain: output position j of the forward
+// transform holds the evaluation at psi^{e_j}, psi = exp(i pi / N),
+// e_j = 4 bitrev9(j) + 1 (mb_exponent), so X^a multiplies it by psi^{a e_j}
+// (a 2N-entry table in LDS). Per pair and wave: the digits of its own ACC
+// component (no rotation and no LDS round trip), L forward transforms, the
+// 3 x 3L row products per subset for its output component, the (psi^{a_S e}
+// - 1) factors, one inverse: about the work of one classic step for two LWE
+// coefficients, at half the barriers.
+namespace fhei {
+namespace mb {
+constexpr int NP_MAX = (v4::NMAX + 1) / 2;  // pairs
+__host__ __device__ constexpr int bitrev9(int j) {
+  int r = 0;
+  for (int b = 0; b < 9; ++b) r |= ((j >> b) & 1) << (8 - b);
+  return r;
+}
+// exponent of output slot u of lane `lane` (layout LC): slot bits are index
+// bits 0-2, so e = ebase(lane) + 256 bitrev3(u), ebase = 4 bitrev9(j(lane, 0)) + 1
+__host__ __device__ constexpr int exponent(int lane, int u) {
+  return (4 * bitrev9(v4::jof(v4::LC, lane, u)) + 1) & 2047;
+}
+// The psi table is stored swizzled, entry x at x ^ ((x >> 4) & 15): the
+// gathers psi^(a e) of a 16-lane group otherwise pile onto a few bank quads
+// (e mod 16 takes 4 values over a group): 38.7 LDS cycles per ds_read_b128
+// on average over a, 8.9 swizzled (4 conflict-free; tools/psi_banks.py).
+__host__ __device__ constexpr int psi_pos(int x) { return x ^ ((x >> 4) & 15); }
+}  // namespace mb
+}  // namespace fhei
+
+// Key-stationary external product: in the product phase wave (g, c) works
+// for output component c of ALL four ciphertexts of the workgroup, on the
+// slot quarter {2g, 2g+1}. Every key element is then loaded once per CU
+// instead of once per ciphertext (4x less L1 traffic, 18 instead of 72 load
+// instructions per wave and level); the products go back to the owning waves
+// through LDS (one more barrier per pair). Measured at 1024 bootstraps:
+// 4.15 ms at (23,1) and 7.4 ms at (15,2), against 5.2 and 12.8 ms with
+// per-ciphertext products and 6.0 / 10.1 ms for the classic v4 kernels.
+//   per pair: digits -> [forward -> F to slot -> barrier -> products for the
+//   quarter -> barrier] x L -> products to the owners' slots -> barrier ->
+//   own slot -> inverse
+// DBG != 0 only in A/B timing builds: 2 = no key loads (wrong results), 128 =
+// phase timestamps of wave DBG >> 8 of workgroup 0, pairs 100..103
+template <int L, int DBG = 0>
+__global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u64* __restrict__ small, int64_t count, int n,
+                                                                      int beta, const c64* __restrict__ bsk,
+                                                                      const c64* __restrict__ tw4,
+                                                                      const c64* __restrict__ psi, BrTv tv, int mode,
+                                                                      u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                                      u64* __restrict__ refreshed, u64* __restrict__ sign) {
+  using namespace v4;
+  using AT = Acc<true>;
+  using T = uint32_t;
+  constexpr int G = 4, NT = nthreads(G), NPSI = 2 * N;
+  constexpr int OFF_TW = NPSI, OFF_X = OFF_TW + NTW, NC64 = OFF_X + G * WPC * SCR;
+  __shared__ c64 lds[NC64];
+  __shared__ uint32_t atab[mb::NP_MAX][G];  // a1 | a2 << 16 per pair and ciphertext
+  c64* psil = lds;
+  c64* twl = lds + OFF_TW;
+  c64* xbuf = lds + OFF_X;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w / WPC, comp = w - g * WPC;
+  const int64_t c = (int64_t)blockIdx.x * G + g;
+  c64* slot = xbuf + (g * WPC + comp) * SCR;
+  T* sa = reinterpret_cast<T*>(slot);
+  const int np = (n + 1) >> 1;
+
+  fill_tables(twl, tw4, tid, NT);
+  for (int x = tid; x < NPSI; x += NT) psil[x] = psi[x];
+  for (int x = tid; x < G * np; x += NT) {
+    const int gg = x / np, jj = x - gg * np;
+    const int64_t cc = (int64_t)blockIdx.x * G + gg;
+    uint32_t a1 = 0, a2 = 0;
+    if (cc < count) {
+      const u64* sm = small + (size_t)cc * (n + 1);
+      a1 = modswitch_2n(sm[2 * jj], 11);
+      if (2 * jj + 1 < n) a2 = modswitch_2n(sm[2 * jj + 1], 11);
+    }
+    atab[jj][gg] = a1 | (a2 << 16);
+  }
+  __syncthreads();
+  const uint32_t ebase = (uint32_t)mb::exponent(lane, 0);
+  // this wave's product quarter: slots 2g, 2g+1 (uniform slot part of e)
+  const uint32_t mq[2] = {(uint32_t)(256 * bitrev3(2 * g)), (uint32_t)(256 * bitrev3(2 * g + 1))};
+
+  T acc[2 * S];
+  {
+    const uint32_t bt = c < count ? modswitch_2n(small[(size_t)c * (n + 1) + n], 11) : 0;
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t idx = (uint32_t)(s * 64 + lane + bt) & (2 * N - 1);
+      acc[s] = comp == K ? AT::from64(tv_rot(tv, idx, N)) : (T)0;
+    }
+  }
+
+  constexpr int R = WPC * L;  // GGSW rows per subset
+  for (int j = 0; j < np; ++j) {
+    [[maybe_unused]] unsigned long long stamp_[16];
+    V4_STAMP(0);
+    uint32_t aS[G][3];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      const uint32_t aa = __builtin_amdgcn_readfirstlane(atab[j][gg]);
+      aS[gg][0] = aa & 0xffffu;
+      aS[gg][1] = aa >> 16;
+      aS[gg][2] = (aS[gg][0] + aS[gg][1]) & (2 * N - 1);
+    }
+    c64 v[S];
+    uint32_t dg[L > 1 ? L - 1 : 1][S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      int d[2][L];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) decompose_v4<L, true>(acc[s + h * S], beta, d[h]);
+      v[s] = {(double)d[0][0], (double)d[1][0]};
+#pragma unroll
+      for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
+    }
+    V4_STAMP(1);
+    c64 o[G][2];  // products of the quarter, per ciphertext
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
+    const c64* Gj = bsk + (size_t)j * 3 * R * WPC * M + (size_t)comp * M + 2 * g * 64 + lane;
+#pragma unroll
+    for (int lv = 0; lv < L; ++lv) {
+      if (lv > 0) {
+#pragma unroll
+        for (int u = 0; u < S; ++u)
+          v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+      }
+      forward(v, twl, slot, lane);
+      V4_STAMP(2 + 4 * lv);
+#pragma unroll
+      for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
+      // key rows of this quarter, slot t: [subset][row] (9 per slot)
+      c64 kb[2][3][WPC];
+      auto load = [&](int t, c64 (&k)[3][WPC]) {
+#pragma unroll
+        for (int Ss = 0; Ss < 3; ++Ss)
+#pragma unroll
+          for (int r = 0; r < WPC; ++r)
+            k[Ss][r] = (DBG & 2) ? c64{0.25 + r, 0.5 * t + Ss}
+                                 : Gj[((size_t)(Ss * R + r * L + lv) * WPC) * M + t * 64];
+      };
+      load(0, kb[0]);
+      V4_STAMP(3 + 4 * lv);
+      lds_barrier();
+      V4_STAMP(4 + 4 * lv);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        // the second slot's rows load when it starts: prefetching them with
+        // the first slot's spilled at L = 2 (10.25 vs 7.36 ms per 1024)
+        if (t == 1) load(1, kb[1]);
+        const int u = 2 * g + t;
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg) {
+          c64 F[WPC];
+#pragma unroll
+          for (int r = 0; r < WPC; ++r) F[r] = xbuf[(gg * WPC + r) * SCR + u * 64 + lane];
+#pragma unroll
+          for (int Ss = 0; Ss < 3; ++Ss) {
+            c64 P = {0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < WPC; ++r) cmac(P, F[r], kb[t][Ss][r]);
+            const uint32_t x = (__umul24(aS[gg][Ss], ebase) + aS[gg][Ss] * mq[t]) & (2 * N - 1);
+            c64 z = psil[mb::psi_pos((int)x)];
+            z.x -= 1.0;
+            cmac(o[gg][t], z, P);
+          }
+        }
+      }
+      V4_STAMP(5 + 4 * lv);
+      lds_barrier();
+    }
+    // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) xbuf[(gg * WPC + comp) * SCR + (2 * g + t) * 64 + lane] = o[gg][t];
+    lds_barrier();
+    V4_STAMP(10);
+    c64 ov[S];
+#pragma unroll
+    for (int u = 0; u < S; ++u) ov[u] = slot[u * 64 + lane];
+    inverse(ov, twl, slot, lane);
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      acc[u] += AT::from_f64(ov[u].x);
+      acc[u + S] += AT::from_f64(ov[u].y);
+    }
+    V4_STAMP(11);
+    if constexpr ((DBG & 128) != 0)
+      if (blockIdx.x == 0 && w == (DBG >> 8) && j >= 100 && j < 104 && lane < 16) {
+        unsigned long long t_ = 0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) t_ = lane == k ? stamp_[k] : t_;
+        g_v4_stamps[j - 100][lane] = t_;
+      }
+  }
+
+  // sample extraction of coefficient 0 (as k_blind_rotate_v4)
+#pragma unroll
+  for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (c < count) {
+    const int W = K * N + 1;
+    if (comp < K) {
+#pragma unroll
+      for (int s = 0; s < 2 * S; ++s) {
+        const int t = s * 64 + lane;
+        const u64 x = t == 0 ? AT::to64(sa[0]) : (u64)0 - AT::to64(sa[N - t]);
+        br_emit(mode, x, false, tv, (size_t)c * W + comp * N + t, out, ct_v, refreshed, sign);
+      }
+    } else if (lane == 0) {
+      br_emit(mode, AT::to64(acc[0]), true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
+    }
+  }
+}
+
+// ---- classic blind rotation with key-stationary products ---------------------
+// k_blind_rotate_v4's step (rotation through the own slot, digits, L forward
+// transforms, one inverse per wave) with the product phase of
+// k_blind_rotate_mb: wave (g, c) forms output component c of all four
+// ciphertexts on the slot quarter {2g, 2g+1}, so each key element is loaded
+// once per CU (6 loads per wave and level instead of 24) and goes back to the
+// owner through LDS (2L + 1 barriers per step instead of 2L).
+template <int L, bool A32, int DBG = 0>
+__global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u64* __restrict__ small, int64_t count, int n,
+                                                                      int beta, const c64* __restrict__ bsk,
+                                                                      const c64* __restrict__ tw4, BrTv tv, int mode,
+                                                                      u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                                      u64* __restrict__ refreshed, u64* __restrict__ sign) {
+  using namespace v4;
+  using AT = Acc<A32>;
+  using T = typename AT::T;
+  constexpr int G = 4, NT = nthreads(G);
+  __shared__ c64 xbuf[G * WPC * SCR];
+  __shared__ c64 twl[NTW];
+  __shared__ uint16_t atab[G][NMAX + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w / WPC, comp = w - g * WPC;
+  const int64_t c = (int64_t)blockIdx.x * G + g;
+  c64* slot = xbuf + (g * WPC + comp) * SCR;
+  T* sa = reinterpret_cast<T*>(slot);
+
+  fill_tables(twl, tw4, tid, NT);
+  for (int x = tid; x < G * (n + 1); x += NT) {
+    const int gg = x / (n + 1), ii = x - gg * (n + 1);
+    const int64_t cc = (int64_t)blockIdx.x * G + gg;
+    atab[gg][ii] = cc < count ? (uint16_t)modswitch_2n(small[(size_t)cc * (n + 1) + ii], 11) : (uint16_t)0;
+  }
+  __syncthreads();
+
+  T acc[2 * S];
+  {
+    const uint32_t bt = atab[g][n];
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t idx = (uint32_t)(s * 64 + lane + bt) & (2 * N - 1);
+      acc[s] = comp == K ? AT::from64(tv_rot(tv, idx, N)) : (T)0;
+    }
+  }
+
+  constexpr int R = WPC * L;
+  // this wave's key column and slot quarter
+  const c64* Gc = bsk + (size_t)comp * M + 2 * g * 64 + lane;
+  auto load = [&](int i, int lv, c64 (&k)[2][WPC]) {
+    const c64* Gi = Gc + (size_t)i * R * WPC * M;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < WPC; ++r)
+        k[t][r] = (DBG & 2) ? c64{0.25 + r, 0.5 * t + lv} : Gi[((size_t)(r * L + lv) * WPC) * M + t * 64];
+  };
+  static_assert(L <= WPC, "key buffers per level");
+  c64 kb[L][2][WPC];  // [level][slot t][row]
+#ifdef FHEICP_V4S_EARLY
+  load(0, 0, kb[0]);
+#endif
+  for (int i = 0; i < n; ++i) {
+    [[maybe_unused]] unsigned long long stamp_[16];
+    V4_STAMP(0);
+    const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)atab[g][i]);
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];  // own slot: in-order DS, no wait
+    c64 v[S];
+    uint32_t dg[L > 1 ? L - 1 : 1][S];
+    T rot[2 * S];
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t src = (uint32_t)(s * 64 + lane - (int)a) & (2 * N - 1);
+      rot[s] = sa[src & (N - 1)];
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      int d[2][L];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
+        const T r = src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S];
+        decompose_v4<L, A32>((T)(r - acc[s + h * S]), beta, d[h]);
+      }
+      v[s] = {(double)d[0][0], (double)d[1][0]};
+#pragma unroll
+      for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
+    }
+    V4_STAMP(1);
+    c64 o[G][2];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
+#pragma unroll
+    for (int lv = 0; lv < L; ++lv) {
+      if (lv > 0) {
+#pragma unroll
+        for (int u = 0; u < S; ++u)
+          v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+      }
+#ifdef FHEICP_V4S_PRE  // A/B: this level's rows fly during its transform
+      load(i, lv, kb[lv]);
+#endif
+      forward(v, twl, slot, lane);
+      V4_STAMP(2 + 4 * lv);
+#pragma unroll
+      for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
+#if !defined(FHEICP_V4S_EARLY) && !defined(FHEICP_V4S_PRE)
+      load(i, lv, kb[lv]);
+#endif
+      V4_STAMP(3 + 4 * lv);
+      lds_barrier();
+      V4_STAMP(4 + 4 * lv);
+#ifdef FHEICP_V4S_EARLY
+      // the next level's (or the next step's first level's) key rows fly
+      // during these products and the next transform
+      if (lv + 1 < L) load(i, lv + 1, kb[lv + 1]);
+      else if (L > 1 && i + 1 < n) load(i + 1, 0, kb[0]);
+#endif
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int u = 2 * g + t;
+#pragma unroll
+        for (int gg = 0; gg < G; ++gg) {
+          c64 F[WPC];
+#pragma unroll
+          for (int r = 0; r < WPC; ++r) F[r] = xbuf[(gg * WPC + r) * SCR + u * 64 + lane];
+#pragma unroll
+          for (int r = 0; r < WPC; ++r) cmac(o[gg][t], F[r], kb[lv][t][r]);
+#ifdef FHEICP_V4S_SB
+          __builtin_amdgcn_sched_barrier(0);  // keep the F reads from all being hoisted (VGPRs)
+#endif
+        }
+      }
+#ifdef FHEICP_V4S_EARLY
+      if (L == 1 && i + 1 < n) load(i + 1, 0, kb[0]);  // after its last use
+#endif
+      V4_STAMP(5 + 4 * lv);
+      lds_barrier();
+    }
+    // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) xbuf[(gg * WPC + comp) * SCR + (2 * g + t) * 64 + lane] = o[gg][t];
+    lds_barrier();
+    V4_STAMP(10);
+    c64 ov[S];
+#pragma unroll
+    for (int u = 0; u < S; ++u) ov[u] = slot[u * 64 + lane];
+    inverse(ov, twl, slot, lane);
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      acc[u] += AT::from_f64(ov[u].x);
+      acc[u + S] += AT::from_f64(ov[u].y);
+    }
+    V4_STAMP(11);
+    if constexpr ((DBG & 128) != 0)
+      if (blockIdx.x == 0 && w == (DBG >> 8) && i >= 100 && i < 104 && lane < 16) {
+        unsigned long long t_ = 0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) t_ = lane == k ? stamp_[k] : t_;
+        g_v4_stamps[i - 100][lane] = t_;
+      }
+  }
+
+#pragma unroll
+  for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (c < count) {
+    const int W = K * N + 1;
+    if (comp < K) {
+#pragma unroll
+      for (int s = 0; s < 2 * S; ++s) {
+        const int t = s * 64 + lane;
+        const u64 x = t == 0 ? AT::to64(sa[0]) : (u64)0 - AT::to64(sa[N - t]);
+        br_emit(mode, x, false, tv, (size_t)c * W + comp * N + t, out, ct_v, refreshed, sign);
+      }
+    } else if (lane == 0) {
+      br_emit(mode, AT::to64(acc[0]), true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
+    }
+  }
+}

@@ -59,6 +59,19 @@ __global__ void __launch_bounds__(256) k_keygen_bsk(ChaKey K, int N, int k, int 
   if (threadIdx.x == 0 && s_small[i]) dst[(size_t)c_in * N] += 1ull << (64 - lvl * beta);
 }
 
+// Messages of the multi-bit bootstrapping key: pair j of the
+// small secret (s1, s2) = (s[2j], s[2j+1]) (s2 = 0 past n) gets three GGSWs,
+// of the indicators s1(1-s2), (1-s1)s2 and s1 s2 (subsets {1}, {2}, {1,2}).
+// k_keygen_bsk then runs with these as its "small secret" (GGSW i = 3j + S).
+__global__ void k_mb_msgs(const u64* __restrict__ s_small, int n, u64* __restrict__ msg) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (n + 1) / 2) return;
+  const u64 s1 = s_small[2 * j], s2 = 2 * j + 1 < n ? s_small[2 * j + 1] : 0;
+  msg[3 * j] = s1 & (1 - s2);
+  msg[3 * j + 1] = (1 - s1) & s2;
+  msg[3 * j + 2] = s1 & s2;
+}
+
 // One workgroup per KSK row (i, l): LWE_{s_small}(s_big[i] * 2^(64 - (l+1) beta)).
 __global__ void __launch_bounds__(256) k_keygen_ksk(ChaKey K, int n, int KL, int kbeta, int noise_bits,
                                                     const u64* __restrict__ s_small, const u64* __restrict__ s_big,

@@ -25,6 +25,10 @@ enum StreamTag : uint32_t {
   TAG_BSK2_NOISE = 10,
   TAG_BSK3_MASK = 11,  // the fast2-gadget bootstrapping key (fhe_params.pbs_fast2_*)
   TAG_BSK3_NOISE = 12,
+  TAG_MB2_MASK = 13,   // the fast gadget's multi-bit key (pairs of LWE coefficients; fhe_params.pbs_fast_group = 2)
+  TAG_MB2_NOISE = 14,
+  TAG_MB3_MASK = 15,   // the fast2 gadget's multi-bit key
+  TAG_MB3_NOISE = 16,
 };
 
 struct ChaKey {

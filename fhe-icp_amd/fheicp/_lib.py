@@ -20,10 +20,11 @@ ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOM
 
 PARAM_FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
                 "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
-                "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level")
+                "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
+                "pbs_fast_group", "pbs_fast2_group")
 # fields a caller may leave out (0 = auto / none)
 OPTIONAL_FIELDS = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log",
-                   "pbs_fast2_level")
+                   "pbs_fast2_level", "pbs_fast_group", "pbs_fast2_group")
 
 
 class FheParams(C.Structure):
@@ -44,6 +45,7 @@ SIGNATURES = [
     ("fhe_get_params", C.c_int, [_CTXP, _P]),
     ("fhe_set_msg_bits", C.c_int, [_CTXP, _i32]),
     ("fhe_bsk_words", C.c_size_t, [_P]),
+    ("fhe_fast_bsk_words", C.c_size_t, [_P, _i32]),
     ("fhe_ksk_words", C.c_size_t, [_P]),
     ("fhe_big_lwe_words", C.c_size_t, [_P]),
     ("fhe_small_lwe_words", C.c_size_t, [_P]),
@@ -60,6 +62,7 @@ SIGNATURES = [
     ("fhe_encrypt_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _u64, _vp, _i64, _vp, _vp]),
     ("fhe_keyswitch_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
     ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
+    ("fhe_pbs_gadget_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
     ("fhe_bit_extract_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp, _vp]),
     ("fhe_sign_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_sign_digit_bits", C.c_int, [_P]),

@@ -90,12 +90,11 @@ class Engine:
         """A fast gadget's bootstrapping key (which = 1: params.pbs_fast_*,
         2: params.pbs_fast2_*)."""
         p = self.params
-        gb, gl = ((p.pbs_fast_base_log, p.pbs_fast_level) if which == 1
-                  else (p.pbs_fast2_base_log, p.pbs_fast2_level))
+        gl = p.pbs_fast_level if which == 1 else p.pbs_fast2_level
         if not gl:
             raise ValueError(f"these parameters have no fast gadget {which}")
-        q = _lib.params_struct({**p.as_dict(), "pbs_base_log": gb, "pbs_level": gl})
-        out = np.zeros(self._L.fhe_bsk_words(C.byref(q)), np.uint64)
+        q = _lib.params_struct(p.as_dict())
+        out = np.zeros(self._L.fhe_fast_bsk_words(C.byref(q), which), np.uint64)
         self._chk(self._L.fhe_export_fast_bsk(self._ctx, which, C.c_void_p(out.ctypes.data)))
         return out
 
@@ -173,6 +172,14 @@ class Engine:
         n = small.numel() // self.Ws
         out = self.empty_big(n)
         self._chk(self._L.fhe_pbs_batch(self._ctx, _ptr(small), n, C.c_uint64(tv), _ptr(out), _stream(self.device)))
+        return out
+
+    def pbs_gadget(self, small: torch.Tensor, gadget: int, tv: int) -> torch.Tensor:
+        """fhe_pbs_batch on gadget 0 (main), 1 (fast) or 2 (fast2) (fhe_pbs_gadget_batch)."""
+        n = small.numel() // self.Ws
+        out = self.empty_big(n)
+        self._chk(self._L.fhe_pbs_gadget_batch(self._ctx, _ptr(small), n, int(gadget), C.c_uint64(tv), _ptr(out),
+                                               _stream(self.device)))
         return out
 
     def pbs_lut(self, small: torch.Tensor, base: int, step: int, log_slots: int) -> torch.Tensor:

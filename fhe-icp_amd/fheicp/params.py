@@ -40,6 +40,10 @@ class SchemeParams:
     # third, cheapest gadget for the last rounds (needs the fast one; 0, 0 = none)
     pbs_fast2_base_log: int = 0
     pbs_fast2_level: int = 0
+    # grouping factor of the fast / fast2 gadget's blind rotation: 0 or 1 =
+    # one LWE coefficient per step, 2 = pairs (multi-bit key)
+    pbs_fast_group: int = 0
+    pbs_fast2_group: int = 0
 
     def as_dict(self) -> dict:
         return asdict(self)
@@ -57,13 +61,17 @@ class SchemeParams:
 # (sign_digit_bits) are used where they too keep 9.2 sigma.
 PBS_GADGETS = ((17, 15, 2), (21, 12, 3), (23, 10, 4), (24, 8, 5), (25, 7, 6), (26, 6, 7), (27, 5, 8))
 SIGMA_BAR = 9.2
-# candidate fast gadgets for the low-amplification sign rounds, and the
-# blind-rotation time per bootstrap by level relative to L = 2, measured on
-# MI355X at 1024 ciphertexts (v4 kernels for L <= 3; L = 1 and 2 on 32-bit
-# accumulators, L = 3 on 64-bit; tools/ab_gadgets.sh): 7.8 / 12.0 / 21 ms.
-# L >= 4 (v2 kernel) is extrapolated; only the ranking matters.
-FAST_GADGETS = ((15, 2), (23, 1))
-BR_COST = {1: 0.65, 2: 1.0, 3: 1.8, 4: 2.6, 5: 3.2, 6: 3.8, 7: 4.4, 8: 5.0}
+# candidate fast gadgets for the low-amplification sign rounds, each with
+# the classic (1) or the multi-bit (2) blind rotation, and the blind-rotation
+# time per bootstrap by (level, group) relative to L = 2 classic, measured on
+# MI355X at 1024 ciphertexts (tools/mb_ab.sh, tools/v4s_ab.sh): classic v4 at
+# L = 1, 2 (32-bit accumulators) 6.0 / 10.1 ms, key-stationary v4s at L = 3
+# (64-bit) 15.9 ms, multi-bit at L = 1, 2: 4.15 / 7.4 ms. L >= 4 (v2 kernel)
+# from C5's 45.7 ms per 1000 at L = 7, the others interpolated; only the
+# ranking matters.
+FAST_GADGETS = ((15, 2, 1), (23, 1, 1), (15, 2, 2), (23, 1, 2))
+BR_COST = {(1, 1): 0.59, (2, 1): 1.0, (3, 1): 1.57, (4, 1): 2.6, (5, 1): 3.2, (6, 1): 3.8, (7, 1): 4.6,
+           (8, 1): 5.2, (1, 2): 0.41, (2, 2): 0.73}
 
 
 def sign_rounds(P: int, d: int):
@@ -85,12 +93,19 @@ def sign_rounds(P: int, d: int):
     return out
 
 
-def _gadget_var(p: "SchemeParams", g: int) -> float:
-    if g == 1 and p.pbs_fast_level:
-        return _variances(replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level))[0]
+def gadget_of(p: "SchemeParams", g: int):
+    """(base_log, level, group) of gadget g: 0 main, 1 fast, 2 fast2 (an
+    absent fast gadget falls back to the previous one, as sign_plan does)."""
     if g == 2 and p.pbs_fast2_level:
-        return _variances(replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level))[0]
-    return _gadget_var(p, g - 1) if g > 0 else _variances(p)[0]
+        return p.pbs_fast2_base_log, p.pbs_fast2_level, max(p.pbs_fast2_group, 1)
+    if g >= 1 and p.pbs_fast_level:
+        return p.pbs_fast_base_log, p.pbs_fast_level, max(p.pbs_fast_group, 1)
+    return p.pbs_base_log, p.pbs_level, 1
+
+
+def _gadget_var(p: "SchemeParams", g: int) -> float:
+    bl, lv, grp = gadget_of(p, g)
+    return _variances(replace(p, pbs_base_log=bl, pbs_level=lv), group=grp)[0]
 
 
 def _plan_worst(p: "SchemeParams", d: int, j1: int, j2: int | None = None) -> float:
@@ -184,10 +199,20 @@ def sign_pbs_count(p) -> int:
     return 2 * (m // d) + (2 if r >= 3 else r) + 1
 
 
+def plan_gadgets(p: SchemeParams) -> list:
+    """(base_log, level, group) of every bootstrap of the sign extraction."""
+    P = p.msg_bits
+    if P < 4:
+        return [gadget_of(p, 0)] * max(P, 0)
+    d, j1, j2 = sign_plan(p)
+    R = len(sign_rounds(P, d))
+    return [gadget_of(p, 0 if r < j1 else 1 if r < j2 else 2) for r in range(R)]
+
+
 def plan_cost(p: SchemeParams) -> float:
     """Relative time of one sign extraction: its bootstraps weighted by
-    BR_COST of the gadget each runs on (sign_plan)."""
-    return sum(BR_COST[lv] for lv in plan_levels(p))
+    BR_COST of the gadget and rotation each runs on (sign_plan)."""
+    return sum(BR_COST[(lv, grp)] for _, lv, grp in plan_gadgets(p))
 
 
 def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
@@ -200,13 +225,13 @@ def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
         if P <= pmax:
             p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
             if fast and P >= 4:
-                cands = [g for g in FAST_GADGETS if g != (beta, lvl)]
-                choices = [(g,) for g in cands] + [(a, b) for i, a in enumerate(cands) for b in cands[i + 1:]]
+                cands = [g for g in FAST_GADGETS if g != (beta, lvl, 1)]
+                choices = [(g,) for g in cands] + [(a, b) for a in cands for b in cands if a[:2] != b[:2]]
                 best = plan_cost(p)
                 for ch in choices:
-                    kw = {"pbs_fast_base_log": ch[0][0], "pbs_fast_level": ch[0][1]}
+                    kw = {"pbs_fast_base_log": ch[0][0], "pbs_fast_level": ch[0][1], "pbs_fast_group": ch[0][2]}
                     if len(ch) > 1:
-                        kw.update(pbs_fast2_base_log=ch[1][0], pbs_fast2_level=ch[1][1])
+                        kw.update(pbs_fast2_base_log=ch[1][0], pbs_fast2_level=ch[1][1], pbs_fast2_group=ch[1][2])
                     q = replace(p, **kw)
                     c = plan_cost(q)
                     if c < best - 1e-9:
@@ -230,9 +255,14 @@ def _tuniform_var(b: int) -> float:
     return (2.0 ** (2 * b + 1) + 1.0) / 6.0
 
 
-def _variances(p: SchemeParams):
+def _variances(p: SchemeParams, group: int = 1):
     """(bootstrap, key switch, modulus switch) output variances, relative to
-    the 2^64 torus."""
+    the 2^64 torus, for the main gadget of p on the classic
+    (group 1) or the multi-bit (group 2) blind rotation: per pair, three GGSWs
+    times (X^a - 1) (3x the key noise), one gadget rounding whose error is
+    multiplied by X^e - 1 (the same total as n classic steps), three subsets'
+    products at |psi^(a e) - 1|^2 ~ 2 (3x the FFT error) and half the 2^32
+    output roundings."""
     q2 = 2.0 ** 128
     s2_bsk = _tuniform_var(p.glwe_noise_bits) / q2
     s2_ksk = _tuniform_var(p.lwe_noise_bits) / q2
@@ -248,6 +278,10 @@ def _variances(p: SchemeParams):
     arith = C_FFT * rows * B * B / 144.0 * 2.0 ** -106
     if p.pbs_base_log * p.pbs_level <= 31:
         arith += 2.0 ** -64 / 12.0
+    if group == 2:
+        fft = C_FFT * rows * B * B / 144.0 * 2.0 ** -106
+        br_key *= 3.0
+        arith = 3.0 * fft + (arith - fft) * 0.5
     v_pbs = br_key + br_round + steps * arith
     Bk = 2.0 ** p.ks_base_log
     v_ks = p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk

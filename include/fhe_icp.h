@@ -66,6 +66,12 @@ typedef struct fhe_params {
                                 re-encrypts it with fresh randomness. */
   int32_t pbs_fast2_base_log; /* optional third, cheapest gadget (0, 0: none; needs the  */
   int32_t pbs_fast2_level;    /* fast one): the rounds from the plan's fast_end on use it */
+  int32_t pbs_fast_group;  /* grouping factor of the fast / fast2 gadget's blind   */
+  int32_t pbs_fast2_group; /* rotation: 0 or 1 = classic, one LWE coefficient per step;
+                              2 = multi-bit, pairs of coefficients with three GGSWs
+                              each (fhe_export_fast_bsk's layout: [pair][subset][row]
+                              [component][coef]); needs N = 1024, k = 2, level <= 2,
+                              level * base_log <= 31 */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;
@@ -102,9 +108,12 @@ int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64
 int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
                     const uint64_t* h_ksk);
 /* a fast gadget's bootstrapping key, which = 1 (pbs_fast_*, stream tags
- * 9/10) or 2 (pbs_fast2_*, tags 11/12): same layout as bsk, fhe_bsk_words of
- * the params with pbs_base_log/pbs_level replaced by that pair. FHE_E_STATE
- * without that gadget. Synchronous. */
+ * 9/10, or 13/14 for a multi-bit key) or 2 (pbs_fast2_*, tags 11/12 or
+ * 15/16): the layout of bsk with one GGSW per LWE coefficient, or three per
+ * pair of coefficients ([pair][subset {1}, {2}, {1,2}][row][component][coef])
+ * when that gadget's group is 2; fhe_fast_bsk_words words (0: no such
+ * gadget). FHE_E_STATE without that gadget. Synchronous. */
+size_t fhe_fast_bsk_words(const fhe_params* params, int32_t which);
 int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk);
 
 /* ---- client side: encrypt / decrypt --------------------------------------
@@ -142,6 +151,13 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
  * extracted under the big key. d_small: count x (n+1); d_out: count x (kN+1). */
 int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t tv, uint64_t* d_out,
                   void* stream);
+/* fhe_pbs_batch on one of the parameter set's gadgets: 0 = the main one
+ * (pbs_base_log, pbs_level), 1 = pbs_fast_*, 2 = pbs_fast2_* (with their own
+ * bootstrapping keys and kernels, e.g. the multi-bit rotation of
+ * pbs_fast_group = 2). FHE_E_STATE if that gadget is
+ * absent. */
+int fhe_pbs_gadget_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, int32_t gadget, uint64_t tv,
+                         uint64_t* d_out, void* stream);
 /* Exact LSB-first bit extraction of the msg_bits-bit value v encrypted in
  * d_ct_v (consumed). d_refreshed receives a fresh encryption of v (sum of
  * the bit ciphertexts), d_sign the ciphertext of the top bit ([v < 0] at

@@ -49,6 +49,8 @@ typedef struct {
   int32_t pbs_fast_level;    /* amplification sign rounds; 0, 0 = none      */
   int32_t pbs_fast2_base_log; /* third, cheapest gadget for the last rounds */
   int32_t pbs_fast2_level;    /* (needs the fast one); 0, 0 = none          */
+  int32_t pbs_fast_group;     /* blind rotation of the fast / fast2 gadget: */
+  int32_t pbs_fast2_group;    /* 0, 1 classic; 2 multi-bit pairs            */
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -128,7 +130,8 @@ int64_t ref_tuniform(uint64_t w, int b) { return tuniform(w, b); }
 
 enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, TAG_KSK_MASK = 5,
        TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10,
-       TAG_BSK3_MASK = 11, TAG_BSK3_NOISE = 12 };
+       TAG_BSK3_MASK = 11, TAG_BSK3_NOISE = 12, TAG_MB2_MASK = 13, TAG_MB2_NOISE = 14, TAG_MB3_MASK = 15,
+       TAG_MB3_NOISE = 16 };
 
 /* --------------------------------------------------- negacyclic product --- */
 /* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
@@ -176,14 +179,16 @@ size_t ref_bsk_words(const ref_params* P) { return (size_t)P->n * rows(P) * (P->
 size_t ref_ksk_words(const ref_params* P) { return (size_t)P->k * P->N * P->ks_level * (P->n + 1); }
 
 /* --------------------------------------------------------------- keygen --- */
-/* BSK rows: GLWE_S(0) + s_small[i] * g_lvl on component c_in, g_lvl = 2^(64 - lvl*beta);
- * (beta, L) and the stream tags select the main or the fast gadget's key */
+/* GGSW i (i < count), row r: GLWE_S(0) + msg[i] * g_lvl on component c_in,
+ * g_lvl = 2^(64 - lvl*beta); (beta, L) and the stream tags select the main or
+ * a fast gadget's key. msg = s_small (one GGSW per LWE coefficient) or the
+ * multi-bit messages of mb_msgs (three per pair). */
 static void bsk_gen(const ref_params* P, const ref_key* Kp, int beta, int L, int tag_mask, int tag_noise,
-                    const uint64_t* s_small, const uint64_t* s_big, uint64_t* bsk) {
+                    const uint64_t* msg, int count, const uint64_t* s_big, uint64_t* bsk) {
   const ref_key K = *Kp;
-  const int n = P->n, k = P->k, N = P->N, R = (k + 1) * L;
+  const int k = P->k, N = P->N, R = (k + 1) * L;
 #pragma omp parallel for schedule(dynamic)
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < count; ++i) {
     uint64_t* scratch = (uint64_t*)malloc(8 * (size_t)(16 * N));
     uint64_t* S = (uint64_t*)malloc(8 * (size_t)N);
     ref_stream sm, sn;
@@ -201,19 +206,37 @@ static void bsk_gen(const ref_params* P, const ref_key* Kp, int beta, int L, int
       }
       stream_init(&sn, &K, tag_noise, (uint64_t)i * R + r);
       for (int t = 0; t < N; ++t) body[t] += (uint64_t)tuniform(stream_word(&sn, (uint64_t)t), P->glwe_noise_bits);
-      if (s_small[i]) row[(size_t)c_in * N] += ((uint64_t)1) << (64 - lvl * beta);
+      if (msg[i]) row[(size_t)c_in * N] += ((uint64_t)1) << (64 - lvl * beta);
     }
     free(scratch);
     free(S);
   }
 }
 
+/* Multi-bit keys (group 2): the LWE coefficients go in
+ * pairs (s1, s2) = (s[2j], s[2j+1]), s2 = 0 past n; pair j has three GGSWs,
+ * of s1(1-s2), (1-s1)s2 and s1 s2 (the subsets {1}, {2}, {1,2}). */
+static int gadget_group(const ref_params* P, int which) {
+  const int g = which == 1 ? P->pbs_fast_group : which == 2 ? P->pbs_fast2_group : 1;
+  return g == 2 ? 2 : 1;
+}
+static int npairs(const ref_params* P) { return (P->n + 1) / 2; }
+static void mb_msgs(const ref_params* P, const uint64_t* s_small, uint64_t* msg) {
+  for (int j = 0; j < npairs(P); ++j) {
+    const uint64_t s1 = s_small[2 * j], s2 = 2 * j + 1 < P->n ? s_small[2 * j + 1] : 0;
+    msg[3 * j] = s1 & (1 - s2);
+    msg[3 * j + 1] = (1 - s1) & s2;
+    msg[3 * j + 2] = s1 & s2;
+  }
+}
 /* a fast gadget's bootstrapping key (fhe_keygen with pbs_fast_* / pbs_fast2_*):
- * same secrets; which = 1: TAG_BSK2_* streams, 2: TAG_BSK3_*; ref_bsk2_words
- * words (the bsk layout of that gadget) */
+ * same secrets; which = 1: TAG_BSK2_* streams (TAG_MB2_* multi-bit), 2:
+ * TAG_BSK3_* (TAG_MB3_*); ref_bsk2_words words (the bsk layout of that
+ * gadget, with 3 GGSWs per pair for a multi-bit key) */
 size_t ref_bsk2_words(const ref_params* P, int which) {
   const int L = which == 1 ? P->pbs_fast_level : P->pbs_fast2_level;
-  return (size_t)P->n * (P->k + 1) * L * (P->k + 1) * P->N;
+  const size_t ggsws = gadget_group(P, which) == 2 ? 3 * (size_t)npairs(P) : (size_t)P->n;
+  return ggsws * (P->k + 1) * L * (P->k + 1) * P->N;
 }
 int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uint64_t* s_small,
                         const uint64_t* s_big, uint64_t* bsk2) {
@@ -221,10 +244,17 @@ int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uin
   if (!L) return -1;
   ref_key K;
   key_from_seed(seed, &K);
-  if (which == 1)
-    bsk_gen(P, &K, P->pbs_fast_base_log, L, TAG_BSK2_MASK, TAG_BSK2_NOISE, s_small, s_big, bsk2);
-  else
-    bsk_gen(P, &K, P->pbs_fast2_base_log, L, TAG_BSK3_MASK, TAG_BSK3_NOISE, s_small, s_big, bsk2);
+  const int bl = which == 1 ? P->pbs_fast_base_log : P->pbs_fast2_base_log;
+  if (gadget_group(P, which) == 2) {
+    uint64_t* msg = (uint64_t*)malloc(8 * 3 * (size_t)npairs(P));
+    mb_msgs(P, s_small, msg);
+    bsk_gen(P, &K, bl, L, which == 1 ? TAG_MB2_MASK : TAG_MB3_MASK, which == 1 ? TAG_MB2_NOISE : TAG_MB3_NOISE, msg,
+            3 * npairs(P), s_big, bsk2);
+    free(msg);
+  } else {
+    bsk_gen(P, &K, bl, L, which == 1 ? TAG_BSK2_MASK : TAG_BSK3_MASK, which == 1 ? TAG_BSK2_NOISE : TAG_BSK3_NOISE,
+            s_small, P->n, s_big, bsk2);
+  }
   return 0;
 }
 
@@ -240,7 +270,7 @@ int ref_keygen(const ref_params* P, uint64_t seed, uint64_t* s_small, uint64_t* 
   stream_init(&st, &K, TAG_SK_GLWE, 0);
   for (int i = 0; i < k * N; ++i) s_big[i] = stream_word(&st, (uint64_t)i) & 1;
 
-  bsk_gen(P, &K, P->pbs_base_log, P->pbs_level, TAG_BSK_MASK, TAG_BSK_NOISE, s_small, s_big, bsk);
+  bsk_gen(P, &K, P->pbs_base_log, P->pbs_level, TAG_BSK_MASK, TAG_BSK_NOISE, s_small, n, s_big, bsk);
 
   /* key-switching key big -> small */
   const int KL = P->ks_level;
@@ -448,10 +478,60 @@ static uint64_t tv_at(const tv_desc* tv, uint32_t idx, int N) {
   return idx < (uint32_t)N ? v : (uint64_t)0 - v;
 }
 
+/* acc += X^a * p - p (negacyclic, a in [0, 2N)) */
+static void add_rot_minus(const uint64_t* p, uint32_t a, int N, uint64_t* acc) {
+  for (int t = 0; t < N; ++t) {
+    const uint32_t idx = (uint32_t)(t - (int)a) & (uint32_t)(2 * N - 1);
+    const uint64_t rot = idx < (uint32_t)N ? p[idx] : (uint64_t)0 - p[idx - N];
+    acc[t] += rot - p[t];
+  }
+}
+
+/* Multi-bit blind rotation (group 2), exact: per pair j with
+ * a1, a2 (a2 = 0 past n) and a12 = a1 + a2 mod 2N,
+ *   G_r = sum_S (X^{a_S} - 1) GGSW_S[r]   (exact, mod 2^64),
+ *   ACC += sum_r digits_r(ACC) * G_r,
+ * the algebra of k_blind_rotate_mb (the GPU forms the same products in the
+ * FFT domain). */
+static void pbs1_mb(const ref_params* P, const uint64_t* bsk, const uint64_t* small, uint64_t* acc, uint64_t* dig,
+                    uint64_t* scratch, uint64_t* G) {
+  const int n = P->n, k = P->k, N = P->N, L = P->pbs_level, R = rows(P), bl = P->pbs_base_log;
+  const int lg = ilog2(2 * N);
+  const size_t ggsw = (size_t)R * (k + 1) * N;
+  int64_t d[64];
+  for (int j = 0; j < npairs(P); ++j) {
+    const uint32_t a1 = modswitch(small[2 * j], lg);
+    const uint32_t a2 = 2 * j + 1 < n ? modswitch(small[2 * j + 1], lg) : 0;
+    const uint32_t aS[3] = {a1, a2, (a1 + a2) & (uint32_t)(2 * N - 1)};
+    if (!a1 && !a2) continue;
+    for (size_t x = 0; x < ggsw; ++x) G[x] = 0;
+    for (int S = 0; S < 3; ++S) {
+      if (!aS[S]) continue;
+      const uint64_t* B = bsk + ((size_t)j * 3 + S) * ggsw;
+      for (size_t q = 0; q < (size_t)R * (k + 1); ++q) add_rot_minus(B + q * N, aS[S], N, G + q * N);
+    }
+    for (int c = 0; c <= k; ++c)
+      for (int t = 0; t < N; ++t) {
+        decompose(acc[(size_t)c * N + t], bl, L, d);
+        for (int l = 0; l < L; ++l) dig[((size_t)c * L + l) * N + t] = (uint64_t)d[l];
+      }
+    for (int r = 0; r < R; ++r)
+      for (int o = 0; o <= k; ++o)
+        negacyclic_mac(dig + (size_t)r * N, G + ((size_t)r * (k + 1) + o) * N, acc + (size_t)o * N, N, scratch);
+  }
+}
+
 /* Bootstrap one small LWE (dim n) with test vector tv; sample extract
- * coefficient 0. out: kN + 1 words under s_big. */
+ * coefficient 0. out: kN + 1 words under s_big. group 2: the multi-bit
+ * rotation with a multi-bit key. */
+static void pbs1g(const ref_params* P, int group, const uint64_t* bsk, const uint64_t* small, const tv_desc* tv,
+                  uint64_t* out, uint64_t* work);
 static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small, const tv_desc* tv, uint64_t* out,
                  uint64_t* work) {
+  pbs1g(P, 1, bsk, small, tv, out, work);
+}
+static void pbs1g(const ref_params* P, int group, const uint64_t* bsk, const uint64_t* small, const tv_desc* tv,
+                  uint64_t* out, uint64_t* work) {
   const int n = P->n, k = P->k, N = P->N, L = P->pbs_level, R = rows(P), bl = P->pbs_base_log;
   const int lg = ilog2(2 * N);
   uint64_t* acc = work;                           /* (k+1)N */
@@ -464,7 +544,8 @@ static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small
     const uint32_t idx = (uint32_t)(t + bt) & (2 * N - 1);
     acc[(size_t)k * N + t] = tv_at(tv, idx, N);
   }
-  for (int i = 0; i < n; ++i) {
+  if (group == 2) pbs1_mb(P, bsk, small, acc, dig, scratch, scratch + 16 * (size_t)N);
+  for (int i = 0; group != 2 && i < n; ++i) {
     const uint32_t ai = modswitch(small[i], lg);
     if (ai == 0) continue;
     /* digits of X^{a_i} ACC - ACC */
@@ -491,7 +572,9 @@ static void pbs1(const ref_params* P, const uint64_t* bsk, const uint64_t* small
   out[(size_t)k * N] = acc[(size_t)k * N];
 }
 static size_t pbs_work_words(const ref_params* P) {
-  return (size_t)(P->k + 1) * P->N + (size_t)rows(P) * P->N + 16 * (size_t)P->N;
+  /* acc | digits | scratch (16N) | the multi-bit combined GGSW (R (k+1) N) */
+  return (size_t)(P->k + 1) * P->N + (size_t)rows(P) * P->N + 16 * (size_t)P->N +
+         (size_t)rows(P) * (P->k + 1) * P->N;
 }
 
 /* Bootstrap count small LWEs with a constant test vector (amplitude tv). */
@@ -504,6 +587,29 @@ void ref_pbs_const(const ref_params* P, const uint64_t* bsk, const uint64_t* sma
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c)
       pbs1(P, bsk, small + (size_t)c * (P->n + 1), &d, out + (size_t)c * (P->k * P->N + 1), work);
+    free(work);
+  }
+}
+
+/* ref_pbs_const on gadget g (fhe_pbs_gadget_batch): 0 = main with bsk, 1 /
+ * 2 = the fast / fast2 gadget with its key from ref_keygen_fast_bsk, on the
+ * classic or the multi-bit rotation by that gadget's group. */
+void ref_pbs_gadget(const ref_params* P0, const uint64_t* bsk, const uint64_t* small, int64_t count, int gadget,
+                    uint64_t tv, uint64_t* out) {
+  ref_params P = *P0;
+  int group = 1;
+  if (gadget == 1 && P.pbs_fast_level) {
+    P.pbs_base_log = P.pbs_fast_base_log; P.pbs_level = P.pbs_fast_level; group = gadget_group(P0, 1);
+  } else if (gadget == 2 && P.pbs_fast2_level) {
+    P.pbs_base_log = P.pbs_fast2_base_log; P.pbs_level = P.pbs_fast2_level; group = gadget_group(P0, 2);
+  }
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(&P));
+    const tv_desc d = {tv, 0, 0, NULL, 0, 0, 0};
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c)
+      pbs1g(&P, group, bsk, small + (size_t)c * (P.n + 1), &d, out + (size_t)c * (P.k * P.N + 1), work);
     free(work);
   }
 }
@@ -588,19 +694,24 @@ void ref_bit_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* k
 /* ------------------------------------------------------------ sign ----- */
 /* One round on ct_v: sh = (ct_v << shift) + add on the body, KS, PBS with tv;
  * mode 1: d = trivial(tv.base) - PBS; mode 2: d = PBS; then ct_v -= d. */
-static void sign_round(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* cv, int shift,
-                       uint64_t add, const tv_desc* tv, int mode, uint64_t* sh, uint64_t* sm, uint64_t* ob,
-                       uint64_t* work) {
+static void sign_round_g(const ref_params* P, int group, const uint64_t* bsk, const uint64_t* ksk, uint64_t* cv,
+                         int shift, uint64_t add, const tv_desc* tv, int mode, uint64_t* sh, uint64_t* sm,
+                         uint64_t* ob, uint64_t* work) {
   const int Wb = P->k * P->N + 1;
   for (int t = 0; t < Wb; ++t) sh[t] = cv[t] << shift;
   sh[Wb - 1] += add;
   keyswitch1(P, ksk, sh, sm);
-  pbs1(P, bsk, sm, tv, ob, work);
+  pbs1g(P, group, bsk, sm, tv, ob, work);
   if (mode == 1) {
     for (int t = 0; t < Wb - 1; ++t) ob[t] = (uint64_t)0 - ob[t];
     ob[Wb - 1] = tv->base - ob[Wb - 1];
   }
   for (int t = 0; t < Wb; ++t) cv[t] -= ob[t];
+}
+static void sign_round(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* cv, int shift,
+                       uint64_t add, const tv_desc* tv, int mode, uint64_t* sh, uint64_t* sm, uint64_t* ob,
+                       uint64_t* work) {
+  sign_round_g(P, 1, bsk, ksk, cv, shift, add, tv, mode, sh, sm, ob, work);
 }
 
 /* Plan of the sign extraction: digit width d and the number
@@ -621,13 +732,22 @@ static double tu_var(int b) { return (ldexp(1.0, 2 * b + 1) + 1.0) / 6.0; }
  * the 2^32 output rounding of the 32-bit-accumulator kernels (L*beta <= 31);
  * both key-weighted like the gadget rounding. */
 #define C_FFT 16.0
-static double pbs_variance(const ref_params* P, int base_log, int L) {
+/* group 2 (multi-bit): three GGSWs per pair, each times
+ * X^a - 1 (3x the key noise), one rounding per pair times X^e - 1 (the same
+ * total), three subsets' products (3x the FFT error), half the 2^32 output
+ * roundings */
+static double pbs_variance(const ref_params* P, int base_log, int L, int group) {
   const double beta = ldexp(1.0, base_log);
   const double rows = (double)L * (P->k + 1) * P->N;
-  const double key = (double)P->n * rows * (beta * beta + 2) / 12.0 * tu_var(P->glwe_noise_bits) / ldexp(1.0, 128);
+  double key = (double)P->n * rows * (beta * beta + 2) / 12.0 * tu_var(P->glwe_noise_bits) / ldexp(1.0, 128);
   const double steps = (double)P->n * (1 + P->k * P->N / 2.0);
-  double arith = C_FFT * rows * beta * beta / 144.0 * ldexp(1.0, -106);
-  if (base_log * L <= 31) arith += ldexp(1.0, -64) / 12.0;
+  const double fft = C_FFT * rows * beta * beta / 144.0 * ldexp(1.0, -106);
+  const double out32 = base_log * L <= 31 ? ldexp(1.0, -64) / 12.0 : 0.0;
+  double arith = fft + out32;
+  if (group == 2) {
+    key *= 3.0;
+    arith = 3.0 * fft + 0.5 * out32;
+  }
   return key + steps / (12.0 * pow(beta, 2.0 * L)) + steps * arith;
 }
 static double fixed_variance(const ref_params* P) {
@@ -655,9 +775,11 @@ static int plan_rounds(int Pb, int d, int* shift, int* mlog) {
 static double plan_margin(const ref_params* P, int d, int j1, int j2) {
   int sh[64], ml[64];
   const int R = plan_rounds(P->msg_bits, d, sh, ml);
-  const double vm = pbs_variance(P, P->pbs_base_log, P->pbs_level);
-  const double vf = P->pbs_fast_level ? pbs_variance(P, P->pbs_fast_base_log, P->pbs_fast_level) : vm;
-  const double vf2 = P->pbs_fast2_level ? pbs_variance(P, P->pbs_fast2_base_log, P->pbs_fast2_level) : vf;
+  const double vm = pbs_variance(P, P->pbs_base_log, P->pbs_level, 1);
+  const double vf =
+      P->pbs_fast_level ? pbs_variance(P, P->pbs_fast_base_log, P->pbs_fast_level, gadget_group(P, 1)) : vm;
+  const double vf2 =
+      P->pbs_fast2_level ? pbs_variance(P, P->pbs_fast2_base_log, P->pbs_fast2_level, gadget_group(P, 2)) : vf;
   const double fx = fixed_variance(P);
   double acc = 0, worst = INFINITY;
   for (int r = 0; r < R; ++r) {
@@ -683,7 +805,7 @@ static void sign_plan(const ref_params* P, int* d_out, int* j1_out, int* j2_out)
     } else {
       /* the worst round of a single-gadget plan: the staircase round of the
        * lowest digit, the preceding bootstrap amplified by 4^(P-d) */
-      const double v = pbs_variance(P, P->pbs_base_log, P->pbs_level) * ldexp(1.0, 2 * (Pb - d4)) +
+      const double v = pbs_variance(P, P->pbs_base_log, P->pbs_level, 1) * ldexp(1.0, 2 * (Pb - d4)) +
                        fixed_variance(P);
       if (ldexp(1.0, -(d4 + 1)) / sqrt(v) >= 9.2) d = d4;
     }
@@ -723,11 +845,12 @@ typedef struct {
   const uint64_t* bsk[3];
   int j1, j2, r;
 } gadget_sched;
-static void sched_next(gadget_sched* g, const ref_params** Pr, const uint64_t** bk) {
+static int sched_next(gadget_sched* g, const ref_params** Pr, const uint64_t** bk) {
   const int r = g->r++;
   const int gi = r < g->j1 ? 0 : r < g->j2 ? 1 : 2;
   *Pr = gi ? &g->Pf[gi - 1] : g->P;
   *bk = g->bsk[gi];
+  return gi ? gadget_group(g->P, gi) : 1;
 }
 
 /* One c-bit digit [b, b+c) of the value in cv: a sign bootstrap of its top bit
@@ -739,11 +862,11 @@ static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int
   const uint64_t* bk;
   const int Pb = g->P->msg_bits, lgN = ilog2(g->P->N);
   const tv_desc hi = {1ull << (62 - Pb + b + c), 0, 0, NULL, 0, 0, 0};
-  sched_next(g, &Pr, &bk);
-  sign_round(Pr, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &hi, 1, sh, sm, ob, work);
+  int grp = sched_next(g, &Pr, &bk);
+  sign_round_g(Pr, grp, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &hi, 1, sh, sm, ob, work);
   const tv_desc lo = {0, 1ull << (64 - Pb + b), lgN - (c - 1), NULL, 0, 0, 0};
-  sched_next(g, &Pr, &bk);
-  sign_round(Pr, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &lo, 2, sh, sm, ob, work);
+  grp = sched_next(g, &Pr, &bk);
+  sign_round_g(Pr, grp, bk, ksk, cv, Pb - b - c, 1ull << (63 - c), &lo, 2, sh, sm, ob, work);
 }
 
 /* Sign of the P-bit value in ct_v with d-bit digits (the
@@ -757,8 +880,8 @@ static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int
 void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* bsk3,
                        const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
   ref_params Pm = *P0;
-  if (!bsk2) Pm.pbs_fast_base_log = Pm.pbs_fast_level = 0;
-  if (!bsk2 || !bsk3) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = 0;
+  if (!bsk2) Pm.pbs_fast_base_log = Pm.pbs_fast_level = Pm.pbs_fast_group = 0;
+  if (!bsk2 || !bsk3) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = Pm.pbs_fast2_group = 0;
   const ref_params* P = &Pm;
   const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
   int d, j1, j2;
@@ -795,12 +918,12 @@ void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t
         }
         for (; b < m; ++b) {
           const tv_desc t = {1ull << (63 - Pb + b), 0, 0, NULL, 0, 0, 0};
-          sched_next(&g, &Pr, &bk);
-          sign_round(Pr, bk, ksk, cv, Pb - b - 1, 1ull << 62, &t, 1, sh, sm, ob, work);
+          const int grp = sched_next(&g, &Pr, &bk);
+          sign_round_g(Pr, grp, bk, ksk, cv, Pb - b - 1, 1ull << 62, &t, 1, sh, sm, ob, work);
         }
         const tv_desc top = {1ull << 62, 0, 0, NULL, 0, 0, 0};
-        sched_next(&g, &Pr, &bk);
-        sign_round(Pr, bk, ksk, cv, 0, 1ull << (63 - d), &top, 1, sh, sm, ob, work);
+        const int grp = sched_next(&g, &Pr, &bk);
+        sign_round_g(Pr, grp, bk, ksk, cv, 0, 1ull << (63 - d), &top, 1, sh, sm, ob, work);
       }
       memcpy(sign + (size_t)c * Wb, ob, 8 * (size_t)Wb);
     }

@@ -17,8 +17,10 @@ _LIB_PATH = _HERE / "build" / "libtfhe_ref.so"
 
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
           "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
-          "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level")
-OPTIONAL = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level")
+          "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
+          "pbs_fast_group", "pbs_fast2_group")
+OPTIONAL = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
+            "pbs_fast_group", "pbs_fast2_group")
 
 
 class RefParams(C.Structure):
@@ -56,6 +58,7 @@ def lib():
         L.ref_keyswitch.argtypes = [P, u64p, u64p, C.c_int64, u64p]
         L.ref_modswitch.argtypes = [P, u64p, C.c_int64, u32p]
         L.ref_pbs_const.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, u64p]
+        L.ref_pbs_gadget.argtypes = [P, u64p, u64p, C.c_int64, C.c_int, C.c_uint64, u64p]
         L.ref_bit_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p, u64p]
         L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
@@ -205,6 +208,16 @@ class RefTFHE:
         cnt = small.size // (self.n + 1)
         out = np.zeros((cnt, self.big + 1), np.uint64)
         lib().ref_pbs_const(C.byref(self.P), u64(self.bsk), u64(small), cnt, C.c_uint64(tv), u64(out))
+        return out
+
+    def pbs_gadget(self, small: np.ndarray, gadget: int, tv: int) -> np.ndarray:
+        """pbs_const on gadget 0 (main), 1 (fast) or 2 (fast2), classic or
+        multi-bit by that gadget's group (fhe_pbs_gadget_batch)."""
+        small = np.ascontiguousarray(small, dtype=np.uint64)
+        cnt = small.size // (self.n + 1)
+        out = np.zeros((cnt, self.big + 1), np.uint64)
+        key = self.bsk if gadget == 0 else self.bsk2 if gadget == 1 else self.bsk3
+        lib().ref_pbs_gadget(C.byref(self.P), u64(key), u64(small), cnt, int(gadget), C.c_uint64(tv), u64(out))
         return out
 
     def pbs_lut(self, small: np.ndarray, base: int, step: int, log_slots: int) -> np.ndarray:

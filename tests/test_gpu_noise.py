@@ -5,11 +5,12 @@ Every decision of the sign extraction is exact only while the noise stays
 inside its margin (>= 9.2 sigma of the model, p_fail <= 2^-64 per bootstrap;
 DESIGN.md §3.5). Sampling a thousand compares cannot show that, so for each
 kernel instance the parameter table can select (v4 32-bit accumulators at
-(15,2) and (23,1), v4 64-bit at (12,3), v2 at levels 4..8) this measures the
-output noise of >= 4096 bootstraps on the real parameters and checks it
-against the model (fheicp.params._variances, the same formula as fheicp.hip
-and oracle/tfhe_ref.c), and checks a few output phases against the exact
-oracle's bootstrap of the same inputs.
+(15,2) and (23,1), the key-stationary v4s with 64-bit accumulators at (12,3),
+v2 at levels 4..8, and the multi-bit rotation of the fast gadgets at (15,2)
+and (23,1)) this measures the output noise of >= 4096 bootstraps on the real
+parameters and checks it against the model (fheicp.params._variances, the
+same formula as fheicp.hip and oracle/tfhe_ref.c), and checks a few output
+phases against the exact oracle's bootstrap of the same inputs.
 """
 import math
 
@@ -17,20 +18,25 @@ import numpy as np
 import pytest
 
 from fheicp.engine import Engine, u64
+from dataclasses import replace
+
 from fheicp.params import SchemeParams, _variances
 
 pytestmark = pytest.mark.gpu
 
-# (base_log, level) -> the instantiation fhe_profile_kernel_name reports
+# (base_log, level, group) -> the instantiation fhe_profile_kernel_name
+# reports; group 2 = the multi-bit rotation, run as a fast gadget
 INSTANCES = {
-    (15, 2): "k_blind_rotate_v4<2, true, 0, 4, false>",
-    (23, 1): "k_blind_rotate_v4<1, true, 0, 4, false>",
-    (12, 3): "k_blind_rotate_v4<3, false, 0, 2, false>",
-    (10, 4): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (8, 5): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (7, 6): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (6, 7): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (5, 8): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (15, 2, 1): "k_blind_rotate_v4<2, true, 0, 4, false>",
+    (23, 1, 1): "k_blind_rotate_v4<1, true, 0, 4, false>",
+    (12, 3, 1): "k_blind_rotate_v4s<3, false, 0>",
+    (10, 4, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (8, 5, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (7, 6, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (6, 7, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (5, 8, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (15, 2, 2): "k_blind_rotate_mb<2, 0>",
+    (23, 1, 2): "k_blind_rotate_mb<1, 0>",
 }
 COUNT = 4096
 TV = 1 << 61
@@ -42,31 +48,37 @@ def signed(x):
 
 @pytest.mark.parametrize("gadget", list(INSTANCES))
 def test_bootstrap_noise_vs_model(need_gpu, oracle_lib, gadget):
-    beta, lvl = gadget
-    prm = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=16)
+    beta, lvl, grp = gadget
+    if grp == 1:
+        prm = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=16)
+    else:   # a fast gadget of a set whose main gadget is (15, 2)
+        prm = SchemeParams(msg_bits=16, pbs_fast_base_log=beta, pbs_fast_level=lvl, pbs_fast_group=2)
+    g = 0 if grp == 1 else 1
+    bucket = "blind_rotate_main" if g == 0 else "blind_rotate_fast"
     eng = Engine(prm, 0)
-    eng.keygen(5000 + 10 * beta + lvl)
+    seed = 5000 + 10 * beta + lvl + 100 * (grp - 1)
+    eng.keygen(seed)
     # inputs at phase +-2^62: far from the 0 / 2^63 boundaries, so the key
     # and modulus switch noise never flips the rotation's half of the torus
     sgn = np.where(np.arange(COUNT) % 2 == 0, 1, -1).astype(np.int64)
     v = sgn * (1 << 14)
     small = eng.keyswitch(eng.encrypt(v, seed=17), 0, 0)
     eng.profile(True)
-    out = eng.pbs(small, TV)
+    out = eng.pbs_gadget(small, g, TV)
     eng.profile(False)
-    assert eng.kernel_name("blind_rotate_main") == INSTANCES[gadget]
-    assert eng.profile_read("blind_rotate_main")["items"] == COUNT
+    assert eng.kernel_name(bucket) == INSTANCES[gadget]
+    assert eng.profile_read(bucket)["items"] == COUNT
     ph = signed(u64(eng.phase(out)))
     err = (ph - sgn * TV).astype(np.float64) / 2.0 ** 64
     sigma = float(np.sqrt(np.mean(err ** 2)))   # RMS: a bias would count too
-    sigma_model = math.sqrt(_variances(prm)[0])
+    sigma_model = math.sqrt(_variances(replace(prm, pbs_base_log=beta, pbs_level=lvl), group=grp)[0])
     print(f"gadget {gadget}: sigma 2^{math.log2(sigma):.2f}, model 2^{math.log2(sigma_model):.2f}, "
           f"max |err| {np.abs(err).max() / sigma_model:.2f} model sigmas")
     assert sigma <= 1.1 * sigma_model
     # the same bootstraps in the exact oracle: phases agree to noise level
-    ref = oracle_lib.RefTFHE(prm.as_dict(), 5000 + 10 * beta + lvl)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), seed)
     sm = u64(small)[:2]
-    ph_ref = signed(ref.phase(ref.pbs_const(sm, TV)))
+    ph_ref = signed(ref.phase(ref.pbs_gadget(sm, g, TV)))
     assert np.abs(ph[:2] - ph_ref).max() < 8 * sigma_model * 2.0 ** 64
     assert np.array_equal(ph_ref > 0, sgn[:2] > 0)
     eng.close()

@@ -224,12 +224,15 @@ def test_sign_toy_all_values_vs_oracle(need_gpu, oracle_lib, P, dbits):
 TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_level=2)
 
 
-@pytest.mark.parametrize("P", [8, 16, 19])
-def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P):
-    """Both bootstrapping keys of a two-gadget parameter set (toy (12,3)+(8,2);
-    real P=16: (15,2)+(23,1); P=19: (12,3)+(15,2)+(23,1)) are bit-exact
-    against the oracle's keygen."""
+@pytest.mark.parametrize("P,grp", [(8, 1), (16, 2), (16, 1), (19, 2)])
+def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
+    """Every bootstrapping key of a multi-gadget parameter set (toy (12,3)+(8,2);
+    real P=16: (15,2) + (15,2) + (23,1); P=19: (12,3) + (15,2) + (23,1)) is
+    bit-exact against the oracle's keygen, the fast gadgets' keys as
+    multi-bit keys (group 2: three GGSWs per pair) and as classic ones."""
     prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 12 else params_for_bits(P)
+    if P >= 12:
+        prm = replace(prm, pbs_fast_group=grp, pbs_fast2_group=grp)
     assert prm.pbs_fast_level
     eng = Engine(prm, 0)
     eng.keygen(4321)
@@ -304,13 +307,17 @@ def test_sign_toy_three_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits):
     eng.close()
 
 
-@pytest.mark.parametrize("P,dbits,fast", [(16, 0, True), (16, 3, True), (19, 0, True), (19, 0, False),
-                                          (21, 0, True), (21, 0, False)])
+@pytest.mark.parametrize("P,dbits,fast", [(16, 0, True), (16, 3, True), (16, 0, "classic"), (19, 0, True),
+                                          (19, 0, False), (21, 0, True), (21, 0, False)])
 def test_sign_real_params(need_gpu, P, dbits, fast):
     """Real parameters at the C2/C4 (P=16: 4-bit digits, and 3-bit forced)
-    and C3 (P=21: 3-bit) widths, with (fast) and without the per-round fast
-    gadget, boundaries included."""
-    eng = Engine(replace(params_for_bits(P, fast=fast), sign_digit_bits=dbits), 0)
+    and C3 (P=21: 3-bit) widths, with (fast; multi-bit fast gadgets) and
+    without the per-round fast gadgets, and with the fast gadgets on the
+    classic rotation ("classic"), boundaries included."""
+    prm = params_for_bits(P, fast=bool(fast))
+    if fast == "classic":
+        prm = replace(prm, pbs_fast_group=1, pbs_fast2_group=1)
+    eng = Engine(replace(prm, sign_digit_bits=dbits), 0)
     eng.keygen(900 + P)
     rng = np.random.default_rng(P)
     h = 2 ** (P - 1)

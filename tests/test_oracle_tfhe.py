@@ -211,6 +211,44 @@ def test_sign_extract_three_gadgets(oracle_lib, P, d):
     assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
 
 
+def test_multibit_rotation_oracle(oracle_lib):
+    """The multi-bit blind rotation (group 2) in the oracle:
+    an odd n (the last pair has a phantom zero coefficient), the key holds
+    three GGSWs per pair, and the bootstrap's output phase equals the classic
+    rotation's to within noise: both rotate the test vector by the same
+    sum_i a_i s_i."""
+    from dataclasses import replace
+    from fheicp.params import TOY
+    prm = replace(TOY, n=63, msg_bits=6, pbs_fast_base_log=15, pbs_fast_level=2, pbs_fast_group=2)
+    r = oracle_lib.RefTFHE(prm.as_dict(), 77)
+    assert r.bsk2.size == 3 * 32 * 3 * 2 * 3 * 256
+    v = np.arange(-32, 32, dtype=np.int64)
+    small = r.keyswitch(r.encrypt_ints(v, seed=9))
+    tv = 1 << 61
+    mb = r.phase(r.pbs_gadget(small, 1, tv)).view(np.int64)
+    cl = r.phase(r.pbs_gadget(small, 0, tv)).view(np.int64)   # classic on the main (15, 2) key
+    assert np.abs(mb - cl).max() < 2 ** 50
+    assert np.array_equal(mb > 0, cl > 0)
+
+
+@pytest.mark.parametrize("P,d", [(6, 3), (8, 4)])
+def test_sign_extract_multibit_gadgets(oracle_lib, P, d):
+    """Sign extraction whose fast and fast2 gadgets run the multi-bit rotation
+    (the real sets' plans, on the toy set): every P-bit value keeps its sign,
+    with the plan the library resolves for these groups."""
+    from dataclasses import replace
+    from fheicp.params import TOY, sign_plan
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=d, pbs_base_log=12, pbs_level=3, pbs_fast_base_log=15,
+                  pbs_fast_level=2, pbs_fast_group=2, pbs_fast2_base_log=23, pbs_fast2_level=1, pbs_fast2_group=2)
+    assert oracle_lib.sign_plan(prm.as_dict()) == sign_plan(prm)
+    assert sign_plan(prm)[2] < P   # rounds on the multi-bit fast2 gadget
+    r = oracle_lib.RefTFHE(prm.as_dict(), 4323)
+    h = 2 ** (P - 1)
+    v = np.arange(-h, h, dtype=np.int64)
+    sign = r.sign_extract(r.encrypt_ints(v, seed=400 + P))
+    assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
+
+
 @pytest.mark.parametrize("lut_bits", [1, 3, 4])
 def test_oracle_pbs_table_every_value(oracle_lib, lut_bits):
     """ref_pbs_table (the restatement of fhe_pbs_table_batch) on the TOY set:

@@ -38,6 +38,8 @@ def _param_sets():
                     yield q.__class__(**{**q.as_dict(), "sign_digit_bits": d})
             for d in (0, 3, 4):
                 yield p.with_msg_bits(P).__class__(**{**p.as_dict(), "sign_digit_bits": d})
+            if fast and p.pbs_fast_level:   # the same gadgets on the classic rotation
+                yield p.__class__(**{**p.as_dict(), "pbs_fast_group": 1, "pbs_fast2_group": 1})
     for P in range(2, 17):
         yield TOY.with_msg_bits(P)
 
@@ -64,22 +66,23 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
 
 
 def test_fast_gadget_plan():
-    """Per-round gadgets: params_for_bits adds the cheapest
-    set of fast gadgets (by BR_COST) for the sign rounds whose noise is barely
-    amplified; only the leading rounds, whose output is shifted up the most,
-    stay on the precise gadget, and every round keeps 9.2 sigma with the
-    fewest main, then fast, rounds."""
+    """Per-round gadgets: params_for_bits adds the
+    cheapest set of fast gadgets (by BR_COST, classic or multi-bit rotation)
+    for the sign rounds whose noise is barely amplified; only the leading
+    rounds, whose output is shifted up the most, stay on the precise gadget,
+    and every round keeps 9.2 sigma with the fewest main, then fast, rounds."""
     from fheicp.params import _plan_worst, plan_cost
-    F, F2 = (15, 2), (23, 1)
-    want = {4: (F2, None, (4, 0, 1)), 9: (F2, None, (4, 0, 4)), 12: (F2, None, (4, 1, 5)),
-            16: (F2, None, (4, 3, 7)), 17: (F2, None, (3, 5, 11)), 18: (F, F2, (4, 1, 5)),
-            19: (F, F2, (4, 1, 5)), 20: (F, F2, (4, 2, 5)), 21: (F, F2, (3, 3, 7)), 22: (F, F2, (3, 3, 8)),
-            23: (F, F2, (3, 4, 9)), 24: (F, F2, (3, 5, 9)), 25: (F, F2, (3, 5, 10)), 26: (F, F2, (3, 6, 11)),
+    F, Fc, F2 = (15, 2, 2), (15, 2, 1), (23, 1, 2)
+    want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F, F2, (4, 0, 1)), 12: (F, F2, (4, 0, 1)),
+            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 1, 3)), 17: (F, F2, (3, 0, 5)), 18: (F, F2, (4, 1, 5)),
+            19: (F, F2, (4, 1, 5)), 20: (Fc, F2, (4, 2, 5)), 21: (F, F2, (3, 3, 7)), 22: (F, F2, (3, 3, 9)),
+            23: (F, F2, (3, 4, 9)), 24: (F, F2, (3, 5, 9)), 25: (F, F2, (3, 5, 11)), 26: (F, F2, (3, 6, 11)),
             27: (F, F2, (3, 7, 11))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
-        assert (p.pbs_fast_base_log, p.pbs_fast_level) == fg, P
-        assert ((p.pbs_fast2_base_log, p.pbs_fast2_level) if p.pbs_fast2_level else None) == fg2, P
+        assert (p.pbs_fast_base_log, p.pbs_fast_level, p.pbs_fast_group) == fg, P
+        got2 = (p.pbs_fast2_base_log, p.pbs_fast2_level, p.pbs_fast2_group) if p.pbs_fast2_level else None
+        assert got2 == fg2, P
         R = len(sign_rounds(P, d))
         assert sign_plan(p) == (d, j1, j2 if fg2 else R), P
         assert _plan_worst(p, d, j1, j2) >= 9.2
@@ -87,10 +90,27 @@ def test_fast_gadget_plan():
         assert fg2 is None or j2 == j1 or _plan_worst(p, d, j1, j2 - 1) < 9.2
         assert R == sign_pbs_count(p)
         assert plan_cost(p) < plan_cost(params_for_bits(P, fast=False))
-    # the headline width keeps its 4-bit digits and the single-gadget worst round
-    assert sign_plan(params_for_bits(16)) == (4, 3, 7)
+    # the headline width keeps its 4-bit digits: one bootstrap on the classic
+    # (15,2) gadget, two on its multi-bit form, four on multi-bit (23,1)
+    assert sign_plan(params_for_bits(16)) == (4, 1, 3)
     assert sign_plan(params_for_bits(19, fast=False)) == (4, 9, 9)
     assert params_for_bits(3).pbs_fast_level == 0
+
+
+def test_multibit_noise_model():
+    """The multi-bit term of the noise model (group 2) is the same formula in
+    params.py, the C library and the oracle (through the plans they resolve),
+    and its factors: 3x key noise, 3x FFT error, half the 2^32 roundings."""
+    from dataclasses import replace
+    from fheicp.params import SchemeParams, _variances
+    for b, lv in ((15, 2), (23, 1)):
+        p = SchemeParams(pbs_base_log=b, pbs_level=lv)
+        v1, v2 = _variances(p)[0], _variances(p, group=2)[0]
+        assert 1.05 < v2 / v1 < 1.8, (b, lv, v2 / v1)
+    # a plan whose fast gadget flips to classic when the group changes differs
+    q = params_for_bits(16)
+    assert q.pbs_fast_group == 2 and q.pbs_fast2_group == 2
+    assert sign_plan(replace(q, pbs_fast_group=1, pbs_fast2_group=1)) != sign_plan(q)
 
 
 def test_sign_digit_bits_validation():
