@@ -342,11 +342,14 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
           const long double ang = 2.0L * PI * (long double)(L * m) / 64.0L;
           t4[v4::NTA + (m - 1) * 8 + L] = {(double)cosl(ang), (double)sinl(ang)};
         }
-      // psi^x = exp(i pi x / N), x < 2N: the monomial factors of the multi-bit rotation
+      // psi^x - 1, psi = exp(i pi / N), x < 2N: the monomial factors of the multi-bit rotation
       std::vector<c64> ps(2 * N);
       for (int x = 0; x < 2 * N; ++x) {
         const long double ang = PI * (long double)x / (long double)N;
-        ps[mb::psi_pos(x)] = {(double)cosl(ang), (double)sinl(ang)};  // bank-swizzled (k_blind_rotate_mb)
+        // psi^x - 1, the factor the products take (cos - 1 = -2 sin^2),
+        // bank-swizzled (k_blind_rotate_mb)
+        const long double h = sinl(ang / 2);
+        ps[mb::psi_pos(x)] = {(double)(-2.0L * h * h), (double)sinl(ang)};
       }
       if (hipMalloc(&ctx->tw4, sizeof(c64) * t4.size()) != hipSuccess ||
           hipMemcpy(ctx->tw4, t4.data(), sizeof(c64) * t4.size(), hipMemcpyHostToDevice) != hipSuccess ||

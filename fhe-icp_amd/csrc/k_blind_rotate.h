@@ -627,7 +627,8 @@ __host__ __device__ constexpr int bitrev9(int j) {
 __host__ __device__ constexpr int exponent(int lane, int u) {
   return (4 * bitrev9(v4::jof(v4::LC, lane, u)) + 1) & 2047;
 }
-// The psi table is stored swizzled, entry x at x ^ ((x >> 4) & 15): the
+// The table holds psi^x - 1 (the factor the products take; cos - 1 as
+// -2 sin^2 for accuracy), stored swizzled, entry x at x ^ ((x >> 4) & 15): the
 // gathers psi^(a e) of a 16-lane group otherwise pile onto a few bank quads
 // (e mod 16 takes 4 values over a group): 38.7 LDS cycles per ds_read_b128
 // on average over a, 8.9 swizzled (4 conflict-free; tools/psi_banks.py).
@@ -736,10 +737,6 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
         for (int u = 0; u < S; ++u)
           v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
       }
-      forward(v, twl, slot, lane);
-      V4_STAMP(2 + 4 * lv);
-#pragma unroll
-      for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
       // key rows of this quarter, slot t: [subset][row] (9 per slot)
       c64 kb[2][3][WPC];
       auto load = [&](int t, c64 (&k)[3][WPC]) {
@@ -750,10 +747,21 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
             k[Ss][r] = (DBG & 2) ? c64{0.25 + r, 0.5 * t + Ss}
                                  : Gj[((size_t)(Ss * R + r * L + lv) * WPC) * M + t * 64];
       };
+      // (loading the first slot's rows before the transform instead, at L = 1:
+      // 4.06 vs 4.04 ms per 1024, not kept)
+      forward(v, twl, slot, lane);
+      V4_STAMP(2 + 4 * lv);
+#pragma unroll
+      for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
       load(0, kb[0]);
       V4_STAMP(3 + 4 * lv);
       lds_barrier();
       V4_STAMP(4 + 4 * lv);
+      // slot 2g+1's exponent is slot 2g's plus 1024 (bitrev3(2g+1) =
+      // bitrev3(2g) + 4): its table position is slot 2g's with bit 10
+      // flipped when a is odd (the swizzle only reads bits 4-7), so the
+      // address is computed once per (ciphertext, subset)
+      uint32_t pa[G][3];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         // the second slot's rows load when it starts: prefetching them with
@@ -770,10 +778,13 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
             c64 P = {0.0, 0.0};
 #pragma unroll
             for (int r = 0; r < WPC; ++r) cmac(P, F[r], kb[t][Ss][r]);
-            const uint32_t x = (__umul24(aS[gg][Ss], ebase) + aS[gg][Ss] * mq[t]) & (2 * N - 1);
-            c64 z = psil[mb::psi_pos((int)x)];
-            z.x -= 1.0;
-            cmac(o[gg][t], z, P);
+            if (t == 0) {
+              const uint32_t x = (__umul24(aS[gg][Ss], ebase) + aS[gg][Ss] * mq[0]) & (2 * N - 1);
+              pa[gg][Ss] = (uint32_t)mb::psi_pos((int)x);
+            } else {
+              pa[gg][Ss] ^= (aS[gg][Ss] & 1u) << 10;
+            }
+            cmac(o[gg][t], psil[pa[gg][Ss]], P);  // the table holds psi^x - 1
           }
         }
       }
