@@ -154,7 +154,7 @@ def read_br(eng) -> dict:
     """Blind-rotation HIP-event totals per gadget (fhe_profile_read) and the
     instantiation each launched (fhe_profile_kernel_name)."""
     out = {}
-    for g in ("main", "fast", "fast2"):
+    for g in ("main", "mid", "mid2", "fast", "fast2"):
         out[g] = eng.profile_read(f"blind_rotate_{g}")
         out[g]["kernel"] = eng.kernel_name(f"blind_rotate_{g}")
     return out
@@ -197,11 +197,14 @@ def roofline(p, brs) -> dict:
     (rocprofv3 SQ_INSTS_VALU_{FMA,ADD,MUL}_F64 of this exact build, x64 lanes,
     FMA x2) / the HIP-event launch time on the kernel's stream. The HBM view
     (algorithmic bytes / time against 8 TB/s, and the PMC-measured bytes as
-    `traffic`) stays beside it. With per-round gadgets two or
-    three kernels run; the one with the largest total time is reported, all
+    `traffic`) stays beside it. With per-round gadgets up to
+    five gadgets run; the kernel with the largest total time is reported, all
     are listed under `kernels`."""
     from dataclasses import replace
     qs = {"main": (p, 1)}
+    for g, bl, lv in (("mid", p.pbs_mid_base_log, p.pbs_mid_level), ("mid2", p.pbs_mid2_base_log, p.pbs_mid2_level)):
+        if lv:
+            qs[g] = (replace(p, pbs_base_log=bl, pbs_level=lv), 1)
     if p.pbs_fast_level:
         qs["fast"] = (replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level),
                       2 if p.pbs_fast_group == 2 else 1)

@@ -43,10 +43,10 @@ struct fhe_ctx {
   u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
   c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr, *tw4 = nullptr;
   c64* bsk_fft_v2 = nullptr;  // v2-layout copy of the main BSK for the table bootstrap (made on first use)
-  // bootstrapping keys of the fast gadgets (p.pbs_fast_*, p.pbs_fast2_*),
-  // coefficient domain and FFT form
-  u64* bskf[2] = {nullptr, nullptr};
-  c64* bskf_fft[2] = {nullptr, nullptr};
+  // bootstrapping keys of the other gadgets (g = 1..4: p.pbs_fast_*,
+  // pbs_fast2_*, pbs_mid_*, pbs_mid2_*), coefficient domain and FFT form
+  u64* bskf[4] = {nullptr, nullptr, nullptr, nullptr};
+  c64* bskf_fft[4] = {nullptr, nullptr, nullptr, nullptr};
   // multi-bit blind rotation of the fast gadgets with pbs_fast*_group = 2
   // (DESIGN.md §4.5): their keys hold three GGSWs per pair of LWE
   // coefficients (messages in mb_msg); psi^x table, x < 2N (bank-swizzled)
@@ -58,7 +58,7 @@ struct fhe_ctx {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool prof = false;
-  ProfAcc prof_br, prof_brf[2], prof_ks;  // blind rotation on the main / fast / fast2 gadget
+  ProfAcc prof_br, prof_brf[4], prof_ks;  // blind rotation on the main / fast / fast2 / mid / mid2 gadget
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2
                        // (two waves per ciphertext; forced by FHEICP_BR_VARIANT=2), 3 (A/B builds)
   // A/B builds only (FHEICP_AB, tools/build_variant.sh): other v4 shapes
@@ -123,6 +123,16 @@ static int validate(const fhe_params* p, std::string& why) {
       (p->pbs_fast2_level && !p->pbs_fast_level)) {
     why = "fast2 pbs decomposition out of range (0, 0 for none; needs a fast gadget)"; return -1;
   }
+  if ((p->pbs_mid_base_log == 0) != (p->pbs_mid_level == 0) || p->pbs_mid_level < 0 || p->pbs_mid_level > 8 ||
+      p->pbs_mid_base_log < 0 || p->pbs_mid_level * p->pbs_mid_base_log > 62 ||
+      (p->pbs_mid_level && !p->pbs_fast_level)) {
+    why = "mid pbs decomposition out of range (0, 0 for none; needs a fast gadget)"; return -1;
+  }
+  if ((p->pbs_mid2_base_log == 0) != (p->pbs_mid2_level == 0) || p->pbs_mid2_level < 0 ||
+      p->pbs_mid2_level > 8 || p->pbs_mid2_base_log < 0 || p->pbs_mid2_level * p->pbs_mid2_base_log > 62 ||
+      (p->pbs_mid2_level && !p->pbs_mid_level)) {
+    why = "mid2 pbs decomposition out of range (0, 0 for none; needs the mid gadget)"; return -1;
+  }
   for (int g = 1; g <= 2; ++g) {
     const int grp = g == 1 ? p->pbs_fast_group : p->pbs_fast2_group;
     const int L = g == 1 ? p->pbs_fast_level : p->pbs_fast2_level;
@@ -136,7 +146,30 @@ static int validate(const fhe_params* p, std::string& why) {
   return 0;
 }
 
-// grouping factor of gadget g's blind rotation (0: main, always 1)
+// The bootstrap gadgets of a parameter set: 0 main (pbs_base_log,
+// pbs_level), 1 fast, 2 fast2, 3 mid, 4 mid2 (0 levels: absent).
+constexpr int NGAD = 5;
+static int gadget_level(const fhe_params& p, int g) {
+  switch (g) {
+    case 0: return p.pbs_level;
+    case 1: return p.pbs_fast_level;
+    case 2: return p.pbs_fast2_level;
+    case 3: return p.pbs_mid_level;
+    case 4: return p.pbs_mid2_level;
+  }
+  return 0;
+}
+static int gadget_base_log(const fhe_params& p, int g) {
+  switch (g) {
+    case 0: return p.pbs_base_log;
+    case 1: return p.pbs_fast_base_log;
+    case 2: return p.pbs_fast2_base_log;
+    case 3: return p.pbs_mid_base_log;
+    case 4: return p.pbs_mid2_base_log;
+  }
+  return 0;
+}
+// grouping factor of gadget g's blind rotation (only fast / fast2 can be 2)
 static int gadget_group(const fhe_params& p, int g) {
   const int v = g == 1 ? p.pbs_fast_group : g == 2 ? p.pbs_fast2_group : 1;
   return v == 2 ? 2 : 1;
@@ -196,59 +229,89 @@ static int sign_rounds(int P, int d, int* shift, int* mlog) {
   add(0, -(d + 1));
   return R;
 }
-// worst margin (sigmas) over all rounds when rounds < j1 use the main gadget,
-// rounds < j2 the fast one and the rest the fast2 one
-static double plan_worst(const fhe_params& p, int d, int j1, int j2) {
+// worst margin (sigmas) over all R rounds when round r runs on gadget sched[r]
+static double plan_worst(const fhe_params& p, int d, const int* sched) {
   int sh[64], ml[64];
   const int R = sign_rounds(p.msg_bits, d, sh, ml);
-  const double vm = pbs_var(p, p.pbs_base_log, p.pbs_level);
-  const double vf = p.pbs_fast_level ? pbs_var(p, p.pbs_fast_base_log, p.pbs_fast_level, gadget_group(p, 1)) : vm;
-  const double vf2 =
-      p.pbs_fast2_level ? pbs_var(p, p.pbs_fast2_base_log, p.pbs_fast2_level, gadget_group(p, 2)) : vf;
+  double var[NGAD];
+  for (int g = 0; g < NGAD; ++g)
+    var[g] = gadget_level(p, g) ? pbs_var(p, gadget_base_log(p, g), gadget_level(p, g), gadget_group(p, g)) : 0.0;
   const double fixed = ks_var(p) + ms_var(p);
   double acc = 0, worst = 1e300;
   for (int r = 0; r < R; ++r) {
     worst = std::min(worst, std::ldexp(1.0, ml[r]) / std::sqrt(acc * std::ldexp(1.0, 2 * sh[r]) + fixed));
-    acc += r < j1 ? vm : r < j2 ? vf : vf2;
+    acc += var[sched[r]];
   }
   // the last bootstrap's output is the sign ciphertext: decryptable at 1/4
-  const double vl = R - 1 < j1 ? vm : R - 1 < j2 ? vf : vf2;
-  return std::min(worst, 0.25 / std::sqrt(vl));
+  return std::min(worst, 0.25 / std::sqrt(var[sched[R - 1]]));
 }
-// (d, j1, j2): digit width; bootstraps < j1 run on the main gadget, < j2 on
-// the fast one, the rest on the fast2 one. Without a fast gadget: the
+// The sign plan: digit width d and the gadget of every
+// bootstrap (sched[0..R), returns R). Without a fast gadget: the
 // single-gadget rule (d = 4 if its worst round keeps 9.2 sigma, else 3), all
 // rounds on the main gadget. With fast gadgets: the widest d (or the forced
-// one), then the fewest main rounds j1 for which some j2 keeps every round at
-// 9.2 sigma, then the fewest fast rounds (j2 = R without a fast2 gadget).
-static void sign_plan(const fhe_params& p, int* d_out, int* j1_out, int* j2_out) {
+// one); then along the ladder main, mid, mid2, fast, fast2 (those present,
+// noisier down the ladder) each gadget takes the fewest leading rounds for
+// which the next gadget on all the remaining ones keeps every decision at 9.2
+// sigma; the last one takes the rest.
+static int sign_schedule(const fhe_params& p, int* d_out, int* sched) {
   int sh[64], ml[64];
   const int P = p.msg_bits;
-  if (P < 4) { *d_out = 0; *j1_out = *j2_out = P; return; }
+  if (P < 4) {
+    *d_out = 0;
+    for (int r = 0; r < P; ++r) sched[r] = 0;
+    return P;
+  }
+  auto all_main = [&](int d) {
+    const int R = sign_rounds(P, d, sh, ml);
+    for (int r = 0; r < R; ++r) sched[r] = 0;
+    *d_out = d;
+    return R;
+  };
   if (!p.pbs_fast_level) {
     int d = 3;
     if (p.sign_digit_bits) d = std::min(p.sign_digit_bits, P);
     else if (digit_margin_sigmas(p, std::min(4, P)) >= 9.2) d = std::min(4, P);
-    *d_out = d;
-    *j1_out = *j2_out = sign_rounds(P, d, sh, ml);
-    return;
+    return all_main(d);
   }
+  int lad[NGAD], m = 0;
+  lad[m++] = 0;
+  for (int g : {3, 4, 1, 2})
+    if (gadget_level(p, g)) lad[m++] = g;
   const int first = p.sign_digit_bits ? std::min(p.sign_digit_bits, P) : std::min(4, P);
   const int last = p.sign_digit_bits ? first : 3;
   for (int d = first; d >= last; --d) {
     const int R = sign_rounds(P, d, sh, ml);
-    for (int j1 = 0; j1 <= R; ++j1) {
-      if (plan_worst(p, d, j1, R) < 9.2) continue;  // fast rounds only help from here
-      int j2 = R;
-      if (p.pbs_fast2_level)
-        for (j2 = j1; j2 < R && plan_worst(p, d, j1, j2) < 9.2; ++j2) {
-        }
-      *d_out = d; *j1_out = j1; *j2_out = j2;
-      return;
+    int start = 0;
+    bool ok = true;
+    for (int i = 0; i + 1 < m; ++i) {
+      int c = start;
+      for (; c <= R; ++c) {
+        for (int r = start; r < R; ++r) sched[r] = r < c ? lad[i] : lad[i + 1];
+        if (plan_worst(p, d, sched) >= 9.2) break;
+      }
+      if (c > R) {  // only when the main gadget alone cannot: a narrower d
+        ok = false;
+        break;
+      }
+      start = c;
+    }
+    if (ok) {
+      *d_out = d;
+      return R;
     }
   }
-  *d_out = last;
-  *j1_out = *j2_out = sign_rounds(P, last, sh, ml);
+  return all_main(last);
+}
+// (d, j1, j2): digit width, the leading main-gadget rounds and the first
+// fast2 round (R without one) of sign_schedule
+static void sign_plan(const fhe_params& p, int* d_out, int* j1_out, int* j2_out) {
+  int sched[64];
+  const int R = sign_schedule(p, d_out, sched);
+  int j1 = 0, j2 = R;
+  while (j1 < R && sched[j1] == 0) ++j1;
+  while (j2 > 0 && sched[j2 - 1] == 2) --j2;
+  *j1_out = j1;
+  *j2_out = j2;
 }
 static int sign_digits(const fhe_params& p) {
   int d, j1, j2;
@@ -387,12 +450,12 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     for (void* ptr : {(void*)ctx->s_small, (void*)ctx->s_big, (void*)ctx->bsk, (void*)ctx->ksk,
                       (void*)ctx->ksk_colsum, (void*)ctx->bsk_fft, (void*)ctx->tw, (void*)ctx->twist, ctx->ws,
                       (void*)ctx->bskf[0], (void*)ctx->bskf[1], (void*)ctx->bskf_fft[0], (void*)ctx->bskf_fft[1],
+                      (void*)ctx->bskf[2], (void*)ctx->bskf[3], (void*)ctx->bskf_fft[2], (void*)ctx->bskf_fft[3],
                       (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2,
                       (void*)ctx->psi, (void*)ctx->mb_msg})
       (void)hipFree(ptr);
     free_ev(ctx->prof_br);
-    free_ev(ctx->prof_brf[0]);
-    free_ev(ctx->prof_brf[1]);
+    for (auto& a : ctx->prof_brf) free_ev(a);
     free_ev(ctx->prof_ks);
   }
   delete ctx;
@@ -433,14 +496,15 @@ static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
     return 2;
   return ctx->br_variant;
 }
-// the parameters seen through fast gadget g (1: pbs_fast_*, 2: pbs_fast2_*;
-// same secret keys, other decomposition and bootstrapping key)
-static int fast_level(const fhe_params& p, int g) { return g == 1 ? p.pbs_fast_level : p.pbs_fast2_level; }
+// the parameters seen through gadget g (1: pbs_fast_*, 2: pbs_fast2_*, 3:
+// pbs_mid_*, 4: pbs_mid2_*; same secret keys, other decomposition and
+// bootstrapping key)
+static int fast_level(const fhe_params& p, int g) { return g >= 1 && g < NGAD ? gadget_level(p, g) : 0; }
 // fast gadget g runs the multi-bit blind rotation
 static bool mb_for(const fhe_params& p, int g) { return g > 0 && fast_level(p, g) && gadget_group(p, g) == 2; }
 static fhe_params fast_params(const fhe_params& p, int g) {
   fhe_params q = p;
-  q.pbs_base_log = g == 1 ? p.pbs_fast_base_log : p.pbs_fast2_base_log;
+  q.pbs_base_log = gadget_base_log(p, g);
   q.pbs_level = fast_level(p, g);
   return q;
 }
@@ -450,15 +514,18 @@ static size_t fast_bsk_words(const fhe_params& p, int g) {
   return (size_t)fast_ggsws(p, g) * (p.k + 1) * fast_level(p, g) * (p.k + 1) * p.N;
 }
 size_t fhe_fast_bsk_words(const fhe_params* p, int32_t which) {
-  if (!p || (which != 1 && which != 2) || !fast_level(*p, which)) return 0;
+  if (!p || which < 1 || which >= NGAD || !fast_level(*p, which)) return 0;
   return fast_bsk_words(*p, which);
 }
-// the fast gadgets' keys under the ChaCha20 streams 9/10 and 11/12 (13/14 and
-// 15/16 for multi-bit keys, whose GGSW messages k_mb_msgs derives)
+// the other gadgets' keys under the ChaCha20 streams 9/10 (fast), 11/12
+// (fast2), 17/18 (mid) and 19/20 (mid2); 13/14 and 15/16 for the fast
+// gadgets' multi-bit keys, whose GGSW messages k_mb_msgs derives
+static const uint32_t kTagMask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK};
+static const uint32_t kTagNoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE};
 static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
   const fhe_params& p = ctx->p;
   const size_t shm = 8 * (size_t)p.N + p.N;
-  for (int g = 1; g <= 2; ++g) {
+  for (int g = 1; g < NGAD; ++g) {
     if (!fast_level(p, g)) continue;
     const fhe_params q = fast_params(p, g);
     const bool mb = mb_for(p, g);
@@ -466,14 +533,13 @@ static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
     hipLaunchKernelGGL(k_keygen_bsk, dim3(fast_ggsws(p, g) * (q.k + 1) * q.pbs_level), dim3(256), shm, st, K, q.N,
                        q.k, q.pbs_level, q.pbs_base_log, q.glwe_noise_bits, mb ? ctx->mb_msg : ctx->s_small,
                        ctx->s_big, ctx->bskf[g - 1],
-                       (uint32_t)(mb ? (g == 1 ? TAG_MB2_MASK : TAG_MB3_MASK) : (g == 1 ? TAG_BSK2_MASK : TAG_BSK3_MASK)),
-                       (uint32_t)(mb ? (g == 1 ? TAG_MB2_NOISE : TAG_MB3_NOISE)
-                                     : (g == 1 ? TAG_BSK2_NOISE : TAG_BSK3_NOISE)));
+                       mb ? (uint32_t)(g == 1 ? TAG_MB2_MASK : TAG_MB3_MASK) : kTagMask[g],
+                       mb ? (uint32_t)(g == 1 ? TAG_MB2_NOISE : TAG_MB3_NOISE) : kTagNoise[g]);
   }
 }
 static int alloc_keys(fhe_ctx* ctx) {
   const fhe_params& p = ctx->p;
-  for (int g = 1; g <= 2; ++g) {
+  for (int g = 1; g < NGAD; ++g) {
     if (!fast_level(p, g) || ctx->bskf[g - 1]) continue;
     const fhe_params q = fast_params(p, g);
     HIPCHK(ctx, hipMalloc(&ctx->bskf[g - 1], 8 * fast_bsk_words(p, g)));
@@ -527,7 +593,7 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
                        ctx->ksk8);
   }
   bsk_to_fft(ctx, p, ctx->bsk, ctx->bsk_fft, st);
-  for (int g = 1; g <= 2; ++g)
+  for (int g = 1; g < NGAD; ++g)
     if (fast_level(p, g))
       bsk_to_fft(ctx, fast_params(p, g), ctx->bskf[g - 1], ctx->bskf_fft[g - 1], st,
                  mb_for(p, g) ? fast_bsk_words(p, g) : 0);
@@ -584,7 +650,8 @@ int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64
 int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk) {
   int rc = need_keys(ctx);
   if (rc) return rc;
-  if (which != 1 && which != 2) return fail(ctx, FHE_E_ARG, "which must be 1 (fast) or 2 (fast2)");
+  if (which < 1 || which >= NGAD)
+    return fail(ctx, FHE_E_ARG, "which must be 1 (fast), 2 (fast2), 3 (mid) or 4 (mid2)");
   if (!fast_level(ctx->p, which)) return fail(ctx, FHE_E_STATE, "no such fast gadget in these parameters");
   if (!h_bsk) return fail(ctx, FHE_E_ARG, "null buffer");
   const fhe_params q = fast_params(ctx->p, which);
@@ -985,7 +1052,7 @@ int fhe_pbs_gadget_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, i
                          uint64_t* d_out, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
-  if (count < 0 || gadget < 0 || gadget > 2 || (count > 0 && (!d_small || !d_out)))
+  if (count < 0 || gadget < 0 || gadget >= NGAD || (count > 0 && (!d_small || !d_out)))
     return fail(ctx, FHE_E_ARG, "bad pbs-gadget arguments");
   if (gadget > 0 && !fast_level(ctx->p, gadget)) return fail(ctx, FHE_E_STATE, "no such fast gadget in these parameters");
   if (count == 0) return FHE_OK;
@@ -1130,6 +1197,16 @@ int fhe_sign_precise_rounds(const fhe_params* params) {
   return j1;
 }
 
+int fhe_sign_schedule(const fhe_params* params, int32_t* gadgets, int32_t cap) {
+  std::string why;
+  if (validate(params, why)) return FHE_E_ARG;
+  int d, sched[64];
+  const int R = sign_schedule(*params, &d, sched);
+  for (int r = 0; r < R && r < cap; ++r)
+    if (gadgets) gadgets[r] = sched[r];
+  return R;
+}
+
 int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_rounds, int32_t* fast_end) {
   std::string why;
   if (validate(params, why)) return FHE_E_ARG;
@@ -1155,14 +1232,12 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
     }
     return FHE_OK;
   }
-  int d, j1, j2;
-  sign_plan(p, &d, &j1, &j2);
+  int d, sched[64];
+  sign_schedule(p, &d, sched);
   const int m = P - d;
-  int round = 0;  // bootstraps issued so far: [0, j1) main, [j1, j2) fast, then fast2 (sign_plan)
+  int round = 0;  // bootstraps issued so far; round r runs on gadget sched[r]
   auto br = [&](BrTv tv, int mode, uint64_t* sign) -> int {
-    const int r = round++;
-    const int gad = r < j1 ? 0 : r < j2 ? 1 : 2;
-    return launch_br(ctx, small, count, tv, mode, nullptr, d_ct_v, nullptr, sign, st, gad);
+    return launch_br(ctx, small, count, tv, mode, nullptr, d_ct_v, nullptr, sign, st, sched[round++]);
   };
   // one c-bit digit at bit b: the pair of rounds on v << (P-b-c) centred by 2^(63-c)
   auto digit = [&](int b, int c) -> int {
@@ -1442,6 +1517,8 @@ static ProfAcc* prof_bucket(fhe_ctx* ctx, const char* kernel) {
   if (!strcmp(kernel, "blind_rotate") || !strcmp(kernel, "blind_rotate_main")) return &ctx->prof_br;
   if (!strcmp(kernel, "blind_rotate_fast")) return &ctx->prof_brf[0];
   if (!strcmp(kernel, "blind_rotate_fast2")) return &ctx->prof_brf[1];
+  if (!strcmp(kernel, "blind_rotate_mid")) return &ctx->prof_brf[2];
+  if (!strcmp(kernel, "blind_rotate_mid2")) return &ctx->prof_brf[3];
   if (!strcmp(kernel, "keyswitch")) return &ctx->prof_ks;
   return nullptr;
 }
@@ -1467,11 +1544,9 @@ int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t
   if (rc) return rc;
   if (!kernel) return fail(ctx, FHE_E_ARG, "null kernel name");
   std::vector<ProfAcc*> acc;
-  if (!strcmp(kernel, "blind_rotate")) acc = {&ctx->prof_br, &ctx->prof_brf[0], &ctx->prof_brf[1]};
-  else if (!strcmp(kernel, "blind_rotate_main")) acc = {&ctx->prof_br};
-  else if (!strcmp(kernel, "blind_rotate_fast")) acc = {&ctx->prof_brf[0]};
-  else if (!strcmp(kernel, "blind_rotate_fast2")) acc = {&ctx->prof_brf[1]};
-  else if (!strcmp(kernel, "keyswitch")) acc = {&ctx->prof_ks};
+  if (!strcmp(kernel, "blind_rotate"))
+    acc = {&ctx->prof_br, &ctx->prof_brf[0], &ctx->prof_brf[1], &ctx->prof_brf[2], &ctx->prof_brf[3]};
+  else if (ProfAcc* a = prof_bucket(ctx, kernel)) acc = {a};
   else return fail(ctx, FHE_E_ARG, "unknown kernel name");
   double ms = 0;
   int64_t nl = 0, it = 0;

@@ -29,6 +29,10 @@ enum StreamTag : uint32_t {
   TAG_MB2_NOISE = 14,
   TAG_MB3_MASK = 15,   // the fast2 gadget's multi-bit key
   TAG_MB3_NOISE = 16,
+  TAG_BSK4_MASK = 17,  // the mid gadget's bootstrapping key (fhe_params.pbs_mid_*)
+  TAG_BSK4_NOISE = 18,
+  TAG_BSK5_MASK = 19,  // the mid2 gadget's bootstrapping key (fhe_params.pbs_mid2_*)
+  TAG_BSK5_NOISE = 20,
 };
 
 struct ChaKey {

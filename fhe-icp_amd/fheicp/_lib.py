@@ -21,10 +21,10 @@ ERRORS = {-1: "FHE_E_ARG", -2: "FHE_E_DEVICE", -3: "FHE_E_STATE", -4: "FHE_E_NOM
 PARAM_FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
                 "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
                 "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
-                "pbs_fast_group", "pbs_fast2_group")
+                "pbs_fast_group", "pbs_fast2_group", "pbs_mid_base_log", "pbs_mid_level",
+                "pbs_mid2_base_log", "pbs_mid2_level")
 # fields a caller may leave out (0 = auto / none)
-OPTIONAL_FIELDS = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log",
-                   "pbs_fast2_level", "pbs_fast_group", "pbs_fast2_group")
+OPTIONAL_FIELDS = PARAM_FIELDS[PARAM_FIELDS.index("sign_digit_bits"):]
 
 
 class FheParams(C.Structure):
@@ -69,6 +69,7 @@ SIGNATURES = [
     ("fhe_sign_pbs_count", C.c_int, [_P]),
     ("fhe_sign_precise_rounds", C.c_int, [_P]),
     ("fhe_sign_plan", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("fhe_sign_schedule", C.c_int, [_P, C.POINTER(C.c_int32), _i32]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_pbs_table_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _i32, _vp, _vp]),
     ("fhe_threshold_batch", C.c_int, [_CTXP, _vp, _i64, _i64, _vp, _vp]),

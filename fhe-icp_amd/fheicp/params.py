@@ -44,6 +44,13 @@ class SchemeParams:
     # one LWE coefficient per step, 2 = pairs (multi-bit key)
     pbs_fast_group: int = 0
     pbs_fast2_group: int = 0
+    # up to two gadgets between the main and the fast one (classic rotation;
+    # 0, 0 = none; mid needs the fast gadget, mid2 needs mid): the sign plan
+    # runs main -> mid -> mid2 -> fast -> fast2 (sign_schedule)
+    pbs_mid_base_log: int = 0
+    pbs_mid_level: int = 0
+    pbs_mid2_base_log: int = 0
+    pbs_mid2_level: int = 0
 
     def as_dict(self) -> dict:
         return asdict(self)
@@ -64,14 +71,14 @@ SIGMA_BAR = 9.2
 # candidate fast gadgets for the low-amplification sign rounds, each with
 # the classic (1) or the multi-bit (2) blind rotation, and the blind-rotation
 # time per bootstrap by (level, group) relative to L = 2 classic, measured on
-# MI355X at 1024 ciphertexts (tools/mb_ab.sh, tools/v4s_ab.sh): classic v4 at
-# L = 1, 2 (32-bit accumulators) 6.0 / 10.1 ms, key-stationary v4s at L = 3
-# (64-bit) 15.9 ms, multi-bit at L = 1, 2: 4.15 / 7.4 ms. L >= 4 (v2 kernel)
-# from C5's 45.7 ms per 1000 at L = 7, the others interpolated; only the
-# ranking matters.
+# MI355X at 1024 ciphertexts (tools/prof_br.py --gadget, tools/lib_ab.sh):
+# classic v4 (32-bit accumulators) L = 1, 2: 6.0 / 9.85 ms; key-stationary
+# v4s (64-bit) L = 3: 15.7 ms; v2 L = 4..8: 29.0 / 34.5 / 40.2 / 45.8 / 51.5
+# ms (prof_br times, 10.9 ms at L = 2 classic); multi-bit L = 1, 2: 4.05 /
+# 6.78 ms. Only the ranking matters.
 FAST_GADGETS = ((15, 2, 1), (23, 1, 1), (15, 2, 2), (23, 1, 2))
-BR_COST = {(1, 1): 0.59, (2, 1): 1.0, (3, 1): 1.57, (4, 1): 2.6, (5, 1): 3.2, (6, 1): 3.8, (7, 1): 4.6,
-           (8, 1): 5.2, (1, 2): 0.41, (2, 2): 0.73}
+BR_COST = {(1, 1): 0.61, (2, 1): 1.0, (3, 1): 1.43, (4, 1): 2.65, (5, 1): 3.16, (6, 1): 3.68, (7, 1): 4.19,
+           (8, 1): 4.71, (1, 2): 0.41, (2, 2): 0.69}
 
 
 def sign_rounds(P: int, d: int):
@@ -93,13 +100,26 @@ def sign_rounds(P: int, d: int):
     return out
 
 
+# gadget ids (fhe_pbs_gadget_batch): 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2
+GADGET_IDS = (0, 1, 2, 3, 4)
+
+
+def gadget_level(p: "SchemeParams", g: int) -> int:
+    return (p.pbs_level, p.pbs_fast_level, p.pbs_fast2_level, p.pbs_mid_level, p.pbs_mid2_level)[g]
+
+
 def gadget_of(p: "SchemeParams", g: int):
-    """(base_log, level, group) of gadget g: 0 main, 1 fast, 2 fast2 (an
-    absent fast gadget falls back to the previous one, as sign_plan does)."""
+    """(base_log, level, group) of gadget g: 0 main, 1 fast, 2 fast2, 3 mid,
+    4 mid2 (an absent fast2 falls back to the fast one, an absent fast, mid or
+    mid2 gadget to the main one)."""
     if g == 2 and p.pbs_fast2_level:
         return p.pbs_fast2_base_log, p.pbs_fast2_level, max(p.pbs_fast2_group, 1)
-    if g >= 1 and p.pbs_fast_level:
+    if g in (1, 2) and p.pbs_fast_level:
         return p.pbs_fast_base_log, p.pbs_fast_level, max(p.pbs_fast_group, 1)
+    if g == 3 and p.pbs_mid_level:
+        return p.pbs_mid_base_log, p.pbs_mid_level, 1
+    if g == 4 and p.pbs_mid2_level:
+        return p.pbs_mid2_base_log, p.pbs_mid2_level, 1
     return p.pbs_base_log, p.pbs_level, 1
 
 
@@ -108,37 +128,48 @@ def _gadget_var(p: "SchemeParams", g: int) -> float:
     return _variances(replace(p, pbs_base_log=bl, pbs_level=lv), group=grp)[0]
 
 
+def _sched_worst(p: "SchemeParams", d: int, sched) -> float:
+    """Worst decision margin (sigmas) when bootstrap r runs on gadget
+    sched[r] (fheicp.hip plan_worst)."""
+    vs = {g: _gadget_var(p, g) for g in set(sched)}
+    _, v_ks, v_ms = _variances(p)
+    acc, worst = 0.0, math.inf
+    for r, (sh, ml) in enumerate(sign_rounds(p.msg_bits, d)):
+        worst = min(worst, 2.0 ** ml / math.sqrt(acc * 4.0 ** sh + v_ks + v_ms))
+        acc += vs[sched[r]]
+    # the last bootstrap's output is the sign ciphertext: decryptable at 1/4
+    return min(worst, 0.25 / math.sqrt(vs[sched[-1]]))
+
+
 def _plan_worst(p: "SchemeParams", d: int, j1: int, j2: int | None = None) -> float:
     """Worst decision margin (sigmas) when bootstraps [0, j1) use the main
     gadget, [j1, j2) the fast one and the rest the fast2 one (j2 = None: all
     the rest on the fast one)."""
-    vs = [_gadget_var(p, g) for g in range(3)]
-    _, v_ks, v_ms = _variances(p)
-    rounds = sign_rounds(p.msg_bits, d)
+    R = len(sign_rounds(p.msg_bits, d))
     if j2 is None:
-        j2 = len(rounds)
-    acc, worst = 0.0, math.inf
-    for r, (sh, ml) in enumerate(rounds):
-        worst = min(worst, 2.0 ** ml / math.sqrt(acc * 4.0 ** sh + v_ks + v_ms))
-        acc += vs[0] if r < j1 else vs[1] if r < j2 else vs[2]
-    # the last bootstrap's output is the sign ciphertext: decryptable at 1/4
-    R = len(rounds)
-    v_last = vs[0] if R - 1 < j1 else vs[1] if R - 1 < j2 else vs[2]
-    return min(worst, 0.25 / math.sqrt(v_last))
+        j2 = R
+    return _sched_worst(p, d, [0 if r < j1 else 1 if r < j2 else 2 for r in range(R)])
 
 
-def sign_plan(p: "SchemeParams"):
-    """(d, j1, j2) of fhe_sign_batch (fhe_sign_plan): digit width d,
-    bootstraps [0, j1) on the main gadget, [j1, j2) on the fast one, the rest
-    on the fast2 one. Without a fast gadget: d = the explicit
+def _ladder(p: "SchemeParams"):
+    """The gadgets the sign plan walks through, in order: main, mid, mid2,
+    fast, fast2 (those present)."""
+    return [0] + [g for g in (3, 4, 1, 2) if gadget_level(p, g)]
+
+
+def sign_schedule(p: "SchemeParams"):
+    """(d, sched) of fhe_sign_batch (fhe_sign_schedule): digit width d and
+    the gadget of every bootstrap. Without a fast gadget: d = the explicit
     p.sign_digit_bits, else 4 if its worst round keeps SIGMA_BAR sigmas, else
     3, and every round on the main gadget. With fast gadgets: the widest d (or
-    the explicit one), then the fewest main rounds j1 for which some j2 keeps
-    every round at SIGMA_BAR, then the fewest fast rounds (j2 = R without a
-    fast2 gadget). (0, P, P) when P < 4 (single-bit rounds)."""
+    the explicit one); then along the ladder main, mid, mid2, fast, fast2 each
+    gadget takes the fewest leading rounds for which the next gadget on all the
+    remaining ones keeps every round at SIGMA_BAR (the ladder's variances grow,
+    so that is the best the rest can do); the last one takes the rest.
+    (0, [0] * P) when P < 4 (single-bit rounds)."""
     P = p.msg_bits
     if P < 4:
-        return 0, P, P
+        return 0, [0] * max(P, 0)
     if p.sign_digit_bits not in (0, 3, 4):
         raise ValueError("sign_digit_bits must be 0 (auto), 3 or 4")
     if not p.pbs_fast_level:
@@ -146,23 +177,39 @@ def sign_plan(p: "SchemeParams"):
             d = min(p.sign_digit_bits, P)
         else:
             d = min(4, P) if _digit_margin(p, min(4, P)) >= SIGMA_BAR else 3
-        R = len(sign_rounds(P, d))
-        return d, R, R
+        return d, [0] * len(sign_rounds(P, d))
+    lad = _ladder(p)
     first = min(p.sign_digit_bits, P) if p.sign_digit_bits else min(4, P)
     last = first if p.sign_digit_bits else 3
     for d in range(first, last - 1, -1):
         R = len(sign_rounds(P, d))
-        for j1 in range(R + 1):
-            if _plan_worst(p, d, j1, R) < SIGMA_BAR:
-                continue
-            j2 = R
-            if p.pbs_fast2_level:
-                j2 = j1
-                while j2 < R and _plan_worst(p, d, j1, j2) < SIGMA_BAR:
-                    j2 += 1
-            return d, j1, j2
-    R = len(sign_rounds(P, last))
-    return last, R, R
+        sched, start, ok = [0] * R, 0, True
+        for i in range(len(lad) - 1):
+            for c in range(start, R + 1):
+                sched[start:] = [lad[i]] * (c - start) + [lad[i + 1]] * (R - c)
+                if _sched_worst(p, d, sched) >= SIGMA_BAR:
+                    break
+            else:
+                ok = False  # the main gadget alone cannot: a narrower d
+                break
+            start = c
+        if ok:
+            return d, sched
+    return last, [0] * len(sign_rounds(P, last))
+
+
+def sign_plan(p: "SchemeParams"):
+    """(d, j1, j2) of fhe_sign_batch (fhe_sign_plan): digit width d, the
+    leading bootstraps [0, j1) on the main gadget and the first fast2 one j2
+    (R without one) of sign_schedule; without mid gadgets, [j1, j2) is the
+    fast gadget's. (0, P, P) when P < 4."""
+    d, sched = sign_schedule(p)
+    R = len(sched)
+    j1 = next((r for r, g in enumerate(sched) if g != 0), R)
+    j2 = R
+    while j2 > 0 and sched[j2 - 1] == 2:
+        j2 -= 1
+    return d, j1, j2
 
 
 def sign_digit_bits(p: "SchemeParams") -> int:
@@ -177,12 +224,7 @@ def sign_precise_rounds(p: "SchemeParams") -> int:
 
 def plan_levels(p: SchemeParams) -> list:
     """Gadget level of every bootstrap of the sign extraction, in order."""
-    P = p.msg_bits
-    if P < 4:
-        return [p.pbs_level] * max(P, 0)
-    d, j1, j2 = sign_plan(p)
-    R = len(sign_rounds(P, d))
-    return [p.pbs_level if r < j1 else p.pbs_fast_level if r < j2 else p.pbs_fast2_level for r in range(R)]
+    return [gadget_of(p, g)[1] for g in sign_schedule(p)[1]]
 
 
 def sign_pbs_count(p) -> int:
@@ -201,12 +243,7 @@ def sign_pbs_count(p) -> int:
 
 def plan_gadgets(p: SchemeParams) -> list:
     """(base_log, level, group) of every bootstrap of the sign extraction."""
-    P = p.msg_bits
-    if P < 4:
-        return [gadget_of(p, 0)] * max(P, 0)
-    d, j1, j2 = sign_plan(p)
-    R = len(sign_rounds(P, d))
-    return [gadget_of(p, 0 if r < j1 else 1 if r < j2 else 2) for r in range(R)]
+    return [gadget_of(p, g) for g in sign_schedule(p)[1]]
 
 
 def plan_cost(p: SchemeParams) -> float:
@@ -220,7 +257,8 @@ def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
     FAST_GADGETS (other than the main gadget, in their order: fast, then
     fast2) for the sign rounds whose noise is barely amplified, the choice
     whose sign plan is cheapest by BR_COST, if it beats the single-gadget
-    plan."""
+    plan; then up to two mid gadgets (cheaper entries of PBS_GADGETS) for the
+    rounds between, if they make the plan cheaper still."""
     for pmax, beta, lvl in PBS_GADGETS:
         if P <= pmax:
             p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
@@ -236,6 +274,19 @@ def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
                     c = plan_cost(q)
                     if c < best - 1e-9:
                         p, best = q, c
+                if p.pbs_fast_level:
+                    # then one or two mid gadgets: cheaper main gadgets of
+                    # PBS_GADGETS, between the main and the fast one
+                    mids = [(b, lv) for _, b, lv in PBS_GADGETS if lv < lvl]
+                    q0 = p
+                    for ch in [(m,) for m in mids] + [(a, b) for a in mids for b in mids if a[1] > b[1]]:
+                        kw = {"pbs_mid_base_log": ch[0][0], "pbs_mid_level": ch[0][1]}
+                        if len(ch) > 1:
+                            kw.update(pbs_mid2_base_log=ch[1][0], pbs_mid2_level=ch[1][1])
+                        q = replace(q0, **kw)
+                        c = plan_cost(q)
+                        if c < best - 1e-9:
+                            p, best = q, c
             return p
     raise ValueError(f"accumulator width P={P} exceeds the supported 27 bits")
 
@@ -315,7 +366,7 @@ def noise_report(p: SchemeParams, method: str = "digits") -> dict:
     margin_sigmas = (2.0 ** -(d + 1) if d > 1 else 0.25) / sigma
     if d > 1 and p.pbs_fast_level:
         # several gadgets: the worst round of sign_plan's schedule
-        margin_sigmas = _plan_worst(p, d, *sign_plan(p)[1:])
+        margin_sigmas = _sched_worst(p, d, sign_schedule(p)[1])
         sigma = 2.0 ** -(d + 1) / margin_sigmas
     return {
         "digit_bits": d if d > 1 else 1,

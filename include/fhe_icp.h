@@ -72,6 +72,13 @@ typedef struct fhe_params {
                               each (fhe_export_fast_bsk's layout: [pair][subset][row]
                               [component][coef]); needs N = 1024, k = 2, level <= 2,
                               level * base_log <= 31 */
+  int32_t pbs_mid_base_log;  /* optional gadgets between the main and the fast one */
+  int32_t pbs_mid_level;     /* (0, 0: none; classic rotation; mid needs the fast  */
+  int32_t pbs_mid2_base_log; /* gadget, mid2 needs mid): the sign plan runs the     */
+  int32_t pbs_mid2_level;    /* rounds main -> mid -> mid2 -> fast -> fast2, each
+                                gadget on the fewest rounds that keep every decision
+                                at 9.2 sigma (fhe_sign_schedule).
+                                Their keys: fhe_export_fast_bsk which = 3, 4. */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;
@@ -108,8 +115,9 @@ int fhe_export_keys(fhe_ctx* ctx, uint64_t* h_s_small, uint64_t* h_s_big, uint64
 int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s_big, const uint64_t* h_bsk,
                     const uint64_t* h_ksk);
 /* a fast gadget's bootstrapping key, which = 1 (pbs_fast_*, stream tags
- * 9/10, or 13/14 for a multi-bit key) or 2 (pbs_fast2_*, tags 11/12 or
- * 15/16): the layout of bsk with one GGSW per LWE coefficient, or three per
+ * 9/10, or 13/14 for a multi-bit key), 2 (pbs_fast2_*, tags 11/12 or
+ * 15/16), 3 (pbs_mid_*, tags 17/18) or 4 (pbs_mid2_*, tags 19/20): the
+ * layout of bsk with one GGSW per LWE coefficient, or three per
  * pair of coefficients ([pair][subset {1}, {2}, {1,2}][row][component][coef])
  * when that gadget's group is 2; fhe_fast_bsk_words words (0: no such
  * gadget). FHE_E_STATE without that gadget. Synchronous. */
@@ -152,7 +160,8 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
 int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t tv, uint64_t* d_out,
                   void* stream);
 /* fhe_pbs_batch on one of the parameter set's gadgets: 0 = the main one
- * (pbs_base_log, pbs_level), 1 = pbs_fast_*, 2 = pbs_fast2_* (with their own
+ * (pbs_base_log, pbs_level), 1 = pbs_fast_*, 2 = pbs_fast2_*, 3 = pbs_mid_*,
+ * 4 = pbs_mid2_* (with their own
  * bootstrapping keys and kernels, e.g. the multi-bit rotation of
  * pbs_fast_group = 2). FHE_E_STATE if that gadget is
  * absent. */
@@ -179,9 +188,14 @@ int fhe_sign_pbs_count(const fhe_params* params);
  * without a fast gadget */
 int fhe_sign_precise_rounds(const fhe_params* params);
 /* the whole plan: digit width, bootstraps [0, main_rounds) on the main
- * gadget, [main_rounds, fast_end) on the fast one, the rest on fast2
+ * gadget, [main_rounds, fast_end) on the mid, mid2 and fast ones (in that
+ * order, fhe_sign_schedule), the rest on fast2
  * (DESIGN.md §3.6). Any pointer may be NULL. */
 int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_rounds, int32_t* fast_end);
+/* the gadget (0..4, as fhe_pbs_gadget_batch) of every bootstrap of
+ * fhe_sign_batch in order, into gadgets[0 .. min(R, cap)); returns R (the
+ * bootstraps per sign extraction) or FHE_E_ARG on bad params. */
+int fhe_sign_schedule(const fhe_params* params, int32_t* gadgets, int32_t cap);
 /* Bootstrap with a staircase test vector over 2^log_slots slots of the half
  * torus: output phase ~ base + floor(phase * 2^log_slots / 2^63) * step for an
  * input phase in [0, 2^63) (negacyclic beyond). log_slots = 0, step = 0 is
@@ -297,9 +311,10 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
  * When enabled, every blind-rotation (external-product) and key-switch
  * launch is bracketed by hipEvents on its own stream. fhe_profile_read
  * synchronises and returns total milliseconds, launch count and ciphertexts
- * processed for kernel "blind_rotate" (both gadgets), "blind_rotate_main",
- * "blind_rotate_fast" (fhe_params.pbs_fast_*) or "keyswitch", then resets
- * what it read. */
+ * processed for kernel "blind_rotate" (all gadgets), "blind_rotate_main",
+ * "blind_rotate_fast" (fhe_params.pbs_fast_*), "blind_rotate_fast2",
+ * "blind_rotate_mid", "blind_rotate_mid2" or "keyswitch", then resets what it
+ * read. */
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
 /* The kernel last launched for that bucket, as rocprofv3 names it (e.g.

@@ -51,6 +51,10 @@ typedef struct {
   int32_t pbs_fast2_level;    /* (needs the fast one); 0, 0 = none          */
   int32_t pbs_fast_group;     /* blind rotation of the fast / fast2 gadget: */
   int32_t pbs_fast2_group;    /* 0, 1 classic; 2 multi-bit pairs            */
+  int32_t pbs_mid_base_log;   /* gadgets between the main and the fast one  */
+  int32_t pbs_mid_level;      /* (classic rotation; 0, 0 = none; mid needs  */
+  int32_t pbs_mid2_base_log;  /* the fast gadget, mid2 needs mid)           */
+  int32_t pbs_mid2_level;
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -131,7 +135,7 @@ int64_t ref_tuniform(uint64_t w, int b) { return tuniform(w, b); }
 enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, TAG_KSK_MASK = 5,
        TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10,
        TAG_BSK3_MASK = 11, TAG_BSK3_NOISE = 12, TAG_MB2_MASK = 13, TAG_MB2_NOISE = 14, TAG_MB3_MASK = 15,
-       TAG_MB3_NOISE = 16 };
+       TAG_MB3_NOISE = 16, TAG_BSK4_MASK = 17, TAG_BSK4_NOISE = 18, TAG_BSK5_MASK = 19, TAG_BSK5_NOISE = 20 };
 
 /* --------------------------------------------------- negacyclic product --- */
 /* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
@@ -220,6 +224,28 @@ static int gadget_group(const ref_params* P, int which) {
   const int g = which == 1 ? P->pbs_fast_group : which == 2 ? P->pbs_fast2_group : 1;
   return g == 2 ? 2 : 1;
 }
+/* gadget `which`: 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2 (level 0: absent) */
+#define NGAD 5
+static int gadget_level(const ref_params* P, int which) {
+  switch (which) {
+    case 0: return P->pbs_level;
+    case 1: return P->pbs_fast_level;
+    case 2: return P->pbs_fast2_level;
+    case 3: return P->pbs_mid_level;
+    case 4: return P->pbs_mid2_level;
+  }
+  return 0;
+}
+static int gadget_base_log(const ref_params* P, int which) {
+  switch (which) {
+    case 0: return P->pbs_base_log;
+    case 1: return P->pbs_fast_base_log;
+    case 2: return P->pbs_fast2_base_log;
+    case 3: return P->pbs_mid_base_log;
+    case 4: return P->pbs_mid2_base_log;
+  }
+  return 0;
+}
 static int npairs(const ref_params* P) { return (P->n + 1) / 2; }
 static void mb_msgs(const ref_params* P, const uint64_t* s_small, uint64_t* msg) {
   for (int j = 0; j < npairs(P); ++j) {
@@ -229,22 +255,25 @@ static void mb_msgs(const ref_params* P, const uint64_t* s_small, uint64_t* msg)
     msg[3 * j + 2] = s1 & s2;
   }
 }
-/* a fast gadget's bootstrapping key (fhe_keygen with pbs_fast_* / pbs_fast2_*):
- * same secrets; which = 1: TAG_BSK2_* streams (TAG_MB2_* multi-bit), 2:
- * TAG_BSK3_* (TAG_MB3_*); ref_bsk2_words words (the bsk layout of that
- * gadget, with 3 GGSWs per pair for a multi-bit key) */
+/* another gadget's bootstrapping key (fhe_keygen with pbs_fast_*,
+ * pbs_fast2_*, pbs_mid_*, pbs_mid2_*): same secrets; which = 1: TAG_BSK2_*
+ * streams (TAG_MB2_* multi-bit), 2: TAG_BSK3_* (TAG_MB3_*), 3: TAG_BSK4_*,
+ * 4: TAG_BSK5_*; ref_bsk2_words words (the bsk layout of that gadget, with 3
+ * GGSWs per pair for a multi-bit key) */
 size_t ref_bsk2_words(const ref_params* P, int which) {
-  const int L = which == 1 ? P->pbs_fast_level : P->pbs_fast2_level;
+  const int L = which >= 1 && which < NGAD ? gadget_level(P, which) : 0;
   const size_t ggsws = gadget_group(P, which) == 2 ? 3 * (size_t)npairs(P) : (size_t)P->n;
   return ggsws * (P->k + 1) * L * (P->k + 1) * P->N;
 }
 int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uint64_t* s_small,
                         const uint64_t* s_big, uint64_t* bsk2) {
-  const int L = which == 1 ? P->pbs_fast_level : which == 2 ? P->pbs_fast2_level : 0;
+  const int L = which >= 1 && which < NGAD ? gadget_level(P, which) : 0;
   if (!L) return -1;
   ref_key K;
   key_from_seed(seed, &K);
-  const int bl = which == 1 ? P->pbs_fast_base_log : P->pbs_fast2_base_log;
+  const int bl = gadget_base_log(P, which);
+  static const int tmask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK};
+  static const int tnoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE};
   if (gadget_group(P, which) == 2) {
     uint64_t* msg = (uint64_t*)malloc(8 * 3 * (size_t)npairs(P));
     mb_msgs(P, s_small, msg);
@@ -252,8 +281,7 @@ int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uin
             3 * npairs(P), s_big, bsk2);
     free(msg);
   } else {
-    bsk_gen(P, &K, bl, L, which == 1 ? TAG_BSK2_MASK : TAG_BSK3_MASK, which == 1 ? TAG_BSK2_NOISE : TAG_BSK3_NOISE,
-            s_small, P->n, s_big, bsk2);
+    bsk_gen(P, &K, bl, L, tmask[which], tnoise[which], s_small, P->n, s_big, bsk2);
   }
   return 0;
 }
@@ -591,17 +619,17 @@ void ref_pbs_const(const ref_params* P, const uint64_t* bsk, const uint64_t* sma
   }
 }
 
-/* ref_pbs_const on gadget g (fhe_pbs_gadget_batch): 0 = main with bsk, 1 /
- * 2 = the fast / fast2 gadget with its key from ref_keygen_fast_bsk, on the
- * classic or the multi-bit rotation by that gadget's group. */
+/* ref_pbs_const on gadget g (fhe_pbs_gadget_batch): 0 = main with bsk, 1..4
+ * = the fast / fast2 / mid / mid2 gadget with its key from
+ * ref_keygen_fast_bsk, on the classic or the multi-bit rotation by that
+ * gadget's group. */
 void ref_pbs_gadget(const ref_params* P0, const uint64_t* bsk, const uint64_t* small, int64_t count, int gadget,
                     uint64_t tv, uint64_t* out) {
   ref_params P = *P0;
   int group = 1;
-  if (gadget == 1 && P.pbs_fast_level) {
-    P.pbs_base_log = P.pbs_fast_base_log; P.pbs_level = P.pbs_fast_level; group = gadget_group(P0, 1);
-  } else if (gadget == 2 && P.pbs_fast2_level) {
-    P.pbs_base_log = P.pbs_fast2_base_log; P.pbs_level = P.pbs_fast2_level; group = gadget_group(P0, 2);
+  if (gadget >= 1 && gadget < NGAD && gadget_level(P0, gadget)) {
+    P.pbs_base_log = gadget_base_log(P0, gadget); P.pbs_level = gadget_level(P0, gadget);
+    group = gadget_group(P0, gadget);
   }
 #pragma omp parallel
   {
@@ -772,64 +800,83 @@ static int plan_rounds(int Pb, int d, int* shift, int* mlog) {
   shift[R] = 0; mlog[R++] = -(d + 1);
   return R;
 }
-static double plan_margin(const ref_params* P, int d, int j1, int j2) {
+/* worst margin (sigmas) when round r runs on gadget sched[r] */
+static double plan_margin(const ref_params* P, int d, const int* sched) {
   int sh[64], ml[64];
   const int R = plan_rounds(P->msg_bits, d, sh, ml);
-  const double vm = pbs_variance(P, P->pbs_base_log, P->pbs_level, 1);
-  const double vf =
-      P->pbs_fast_level ? pbs_variance(P, P->pbs_fast_base_log, P->pbs_fast_level, gadget_group(P, 1)) : vm;
-  const double vf2 =
-      P->pbs_fast2_level ? pbs_variance(P, P->pbs_fast2_base_log, P->pbs_fast2_level, gadget_group(P, 2)) : vf;
+  double var[NGAD];
+  for (int g = 0; g < NGAD; ++g)
+    var[g] = gadget_level(P, g) ? pbs_variance(P, gadget_base_log(P, g), gadget_level(P, g), gadget_group(P, g)) : 0.0;
   const double fx = fixed_variance(P);
   double acc = 0, worst = INFINITY;
   for (int r = 0; r < R; ++r) {
     const double m = ldexp(1.0, ml[r]) / sqrt(acc * ldexp(1.0, 2 * sh[r]) + fx);
     if (m < worst) worst = m;
-    acc += r < j1 ? vm : r < j2 ? vf : vf2;
+    acc += var[sched[r]];
   }
   /* the last bootstrap's output is the sign ciphertext: decryptable at 1/4 */
-  const double vl = R - 1 < j1 ? vm : R - 1 < j2 ? vf : vf2;
-  const double ml_last = 0.25 / sqrt(vl);
+  const double ml_last = 0.25 / sqrt(var[sched[R - 1]]);
   return ml_last < worst ? ml_last : worst;
 }
-/* (d, j1, j2): bootstraps [0, j1) on the main gadget, [j1, j2) on the fast
- * one, the rest on fast2 */
-static void sign_plan(const ref_params* P, int* d_out, int* j1_out, int* j2_out) {
+/* The plan: digit width d and the gadget of every bootstrap (sched, returns
+ * R). With fast gadgets, along the ladder main, mid, mid2, fast, fast2 (those
+ * present) each gadget takes the fewest leading rounds for which the next one
+ * on all remaining rounds keeps every decision at 9.2 sigma; the last takes
+ * the rest. */
+static int sign_schedule(const ref_params* P, int* d_out, int* sched) {
   int sh[64], ml[64];
   const int Pb = P->msg_bits, d4 = Pb < 4 ? Pb : 4;
-  if (Pb < 4) { *d_out = 0; *j1_out = *j2_out = Pb; return; }
-  if (!P->pbs_fast_level) {
-    int d = 3;
-    if (P->sign_digit_bits) {
-      d = P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb;
-    } else {
-      /* the worst round of a single-gadget plan: the staircase round of the
-       * lowest digit, the preceding bootstrap amplified by 4^(P-d) */
-      const double v = pbs_variance(P, P->pbs_base_log, P->pbs_level, 1) * ldexp(1.0, 2 * (Pb - d4)) +
-                       fixed_variance(P);
-      if (ldexp(1.0, -(d4 + 1)) / sqrt(v) >= 9.2) d = d4;
-    }
-    *d_out = d;
-    *j1_out = *j2_out = plan_rounds(Pb, d, sh, ml);
-    return;
+  if (Pb < 4) {
+    *d_out = 0;
+    for (int r = 0; r < Pb; ++r) sched[r] = 0;
+    return Pb;
   }
-  const int first = P->sign_digit_bits ? (P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb) : d4;
-  const int last = P->sign_digit_bits ? first : 3;
-  for (int d = first; d >= last; --d) {
-    const int R = plan_rounds(Pb, d, sh, ml);
-    for (int j1 = 0; j1 <= R; ++j1) {
-      if (plan_margin(P, d, j1, R) < 9.2) continue;
-      int j2 = R;
-      if (P->pbs_fast2_level) {
-        j2 = j1;
-        while (j2 < R && plan_margin(P, d, j1, j2) < 9.2) ++j2;
+  int dd = 3;
+  if (P->pbs_fast_level) {
+    int lad[NGAD], m = 0;
+    const int order[4] = {3, 4, 1, 2};
+    lad[m++] = 0;
+    for (int i = 0; i < 4; ++i)
+      if (gadget_level(P, order[i])) lad[m++] = order[i];
+    const int first = P->sign_digit_bits ? (P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb) : d4;
+    const int last = P->sign_digit_bits ? first : 3;
+    for (int d = first; d >= last; --d) {
+      const int R = plan_rounds(Pb, d, sh, ml);
+      int start = 0, ok = 1;
+      for (int i = 0; i + 1 < m; ++i) {
+        int c = start;
+        for (; c <= R; ++c) {
+          for (int r = start; r < R; ++r) sched[r] = r < c ? lad[i] : lad[i + 1];
+          if (plan_margin(P, d, sched) >= 9.2) break;
+        }
+        if (c > R) { ok = 0; break; } /* the main gadget alone cannot: narrower d */
+        start = c;
       }
-      *d_out = d; *j1_out = j1; *j2_out = j2;
-      return;
+      if (ok) { *d_out = d; return R; }
     }
+    dd = last;
+  } else if (P->sign_digit_bits) {
+    dd = P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb;
+  } else {
+    /* the worst round of a single-gadget plan: the staircase round of the
+     * lowest digit, the preceding bootstrap amplified by 4^(P-d) */
+    const double v = pbs_variance(P, P->pbs_base_log, P->pbs_level, 1) * ldexp(1.0, 2 * (Pb - d4)) + fixed_variance(P);
+    if (ldexp(1.0, -(d4 + 1)) / sqrt(v) >= 9.2) dd = d4;
   }
-  *d_out = last;
-  *j1_out = *j2_out = plan_rounds(Pb, last, sh, ml);
+  *d_out = dd;
+  const int R = plan_rounds(Pb, dd, sh, ml);
+  for (int r = 0; r < R; ++r) sched[r] = 0;
+  return R;
+}
+/* (d, j1, j2): the leading main-gadget bootstraps j1 and the first fast2
+ * one j2 (R without one) of sign_schedule */
+static void sign_plan(const ref_params* P, int* d_out, int* j1_out, int* j2_out) {
+  int sched[64];
+  const int R = sign_schedule(P, d_out, sched);
+  int j1 = 0, j2 = R;
+  while (j1 < R && sched[j1] == 0) ++j1;
+  while (j2 > 0 && sched[j2 - 1] == 2) --j2;
+  *j1_out = j1; *j2_out = j2;
 }
 static int digit_bits(const ref_params* P) {
   int d, j1, j2;
@@ -837,17 +884,16 @@ static int digit_bits(const ref_params* P) {
   return d;
 }
 
-/* the bootstrap gadget and key of round r: main for r < j1, fast for r < j2,
- * else fast2 */
+/* the bootstrap gadget and key of the next round (sign_schedule) */
 typedef struct {
   const ref_params* P;
-  ref_params Pf[2]; /* P seen through the fast / fast2 gadget */
-  const uint64_t* bsk[3];
-  int j1, j2, r;
+  ref_params Pf[NGAD - 1]; /* P seen through gadget 1..4 */
+  const uint64_t* bsk[NGAD];
+  int sched[64];
+  int r;
 } gadget_sched;
 static int sched_next(gadget_sched* g, const ref_params** Pr, const uint64_t** bk) {
-  const int r = g->r++;
-  const int gi = r < g->j1 ? 0 : r < g->j2 ? 1 : 2;
+  const int gi = g->sched[g->r++];
   *Pr = gi ? &g->Pf[gi - 1] : g->P;
   *bk = g->bsk[gi];
   return gi ? gadget_group(g->P, gi) : 1;
@@ -874,23 +920,34 @@ static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int
  * digits [b, b+d) by digit_rounds, a leftover of >= 3 bits as one shorter
  * digit, of 1-2 bits by single-bit rounds; then the sign of the top d bits
  * (centred by 2^(63-d), tv 2^62). sign[count x (kN+1)] encrypts [v < 0] at
- * 2^63; ct_v is consumed. With fast gadgets (P->pbs_fast_*, P->pbs_fast2_*) and
- * their keys bsk2, bsk3, bootstraps [j1, j2) of sign_plan use the fast one and
- * the rest the fast2 one; a NULL key plans as if that gadget were not set. */
-void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* bsk3,
-                       const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
+ * 2^63; ct_v is consumed. keys[g - 1] is the key of gadget g = 1..4 (fast,
+ * fast2, mid, mid2); round r runs on gadget sign_schedule[r]; a NULL key
+ * plans as if that gadget were not set (with the ones that need it). */
+void ref_sign_extract_keys(const ref_params* P0, const uint64_t* bsk, const uint64_t* const* keys,
+                           const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
   ref_params Pm = *P0;
-  if (!bsk2) Pm.pbs_fast_base_log = Pm.pbs_fast_level = Pm.pbs_fast_group = 0;
-  if (!bsk2 || !bsk3) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = Pm.pbs_fast2_group = 0;
+  if (!keys[0]) Pm.pbs_fast_base_log = Pm.pbs_fast_level = Pm.pbs_fast_group = 0;
+  if (!keys[0] || !keys[1]) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = Pm.pbs_fast2_group = 0;
+  if (!keys[0] || !keys[2]) Pm.pbs_mid_base_log = Pm.pbs_mid_level = 0;
+  if (!Pm.pbs_mid_level || !keys[3]) Pm.pbs_mid2_base_log = Pm.pbs_mid2_level = 0;
   const ref_params* P = &Pm;
   const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
-  int d, j1, j2;
-  sign_plan(P, &d, &j1, &j2);
-  ref_params Pf[2] = {*P, *P};
-  if (P->pbs_fast_level) { Pf[0].pbs_base_log = P->pbs_fast_base_log; Pf[0].pbs_level = P->pbs_fast_level; }
-  if (P->pbs_fast2_level) { Pf[1].pbs_base_log = P->pbs_fast2_base_log; Pf[1].pbs_level = P->pbs_fast2_level; }
+  gadget_sched g0;
+  g0.P = P;
+  g0.r = 0;
+  g0.bsk[0] = bsk;
+  int d;
+  sign_schedule(P, &d, g0.sched);
   size_t ww = pbs_work_words(P);
-  for (int g = 0; g < 2; ++g) if (pbs_work_words(&Pf[g]) > ww) ww = pbs_work_words(&Pf[g]);
+  for (int g = 1; g < NGAD; ++g) {
+    g0.Pf[g - 1] = *P;
+    g0.bsk[g] = keys[g - 1];
+    if (gadget_level(P, g)) {
+      g0.Pf[g - 1].pbs_base_log = gadget_base_log(P, g);
+      g0.Pf[g - 1].pbs_level = gadget_level(P, g);
+    }
+    if (pbs_work_words(&g0.Pf[g - 1]) > ww) ww = pbs_work_words(&g0.Pf[g - 1]);
+  }
 #pragma omp parallel
   {
     uint64_t* work = (uint64_t*)malloc(8 * ww);
@@ -900,7 +957,7 @@ void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t
 #pragma omp for schedule(dynamic)
     for (int64_t c = 0; c < count; ++c) {
       uint64_t* cv = ct_v + (size_t)c * Wb;
-      gadget_sched g = {P, {Pf[0], Pf[1]}, {bsk, bsk2, bsk3}, j1, j2, 0};
+      gadget_sched g = g0;
       const ref_params* Pr;
       const uint64_t* bk;
       if (Pb < 4) {
@@ -930,6 +987,11 @@ void ref_sign_extract3(const ref_params* P0, const uint64_t* bsk, const uint64_t
     free(work); free(sh); free(sm); free(ob);
   }
 }
+void ref_sign_extract3(const ref_params* P, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* bsk3,
+                       const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
+  const uint64_t* keys[4] = {bsk2, bsk3, NULL, NULL};
+  ref_sign_extract_keys(P, bsk, keys, ksk, ct_v, count, sign);
+}
 void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,
                       uint64_t* sign) {
   ref_sign_extract3(P, bsk, NULL, NULL, ksk, ct_v, count, sign);
@@ -939,6 +1001,12 @@ int ref_sign_precise_rounds(const ref_params* P) {
   int d, j1, j2;
   sign_plan(P, &d, &j1, &j2);
   return j1;
+}
+int ref_sign_schedule(const ref_params* P, int32_t* out, int32_t cap) {
+  int d, sched[64];
+  const int R = sign_schedule(P, &d, sched);
+  for (int r = 0; r < R && r < cap; ++r) out[r] = sched[r];
+  return R;
 }
 void ref_sign_plan(const ref_params* P, int32_t* d, int32_t* j1, int32_t* j2) {
   int a, b, c;

@@ -18,9 +18,11 @@ _LIB_PATH = _HERE / "build" / "libtfhe_ref.so"
 FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
           "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
           "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
-          "pbs_fast_group", "pbs_fast2_group")
-OPTIONAL = ("sign_digit_bits", "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
-            "pbs_fast_group", "pbs_fast2_group")
+          "pbs_fast_group", "pbs_fast2_group", "pbs_mid_base_log", "pbs_mid_level", "pbs_mid2_base_log",
+          "pbs_mid2_level")
+OPTIONAL = FIELDS[FIELDS.index("sign_digit_bits"):]
+# gadget g = 1..4 (fast, fast2, mid, mid2) and the level field that enables it
+GADGET_LEVEL = {1: "pbs_fast_level", 2: "pbs_fast2_level", 3: "pbs_mid_level", 4: "pbs_mid2_level"}
 
 
 class RefParams(C.Structure):
@@ -64,6 +66,8 @@ def lib():
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
         L.ref_pbs_table.argtypes = [P, u64p, u64p, C.c_int64, i64p, C.c_int, u64p]
         L.ref_sign_extract3.argtypes = [P, u64p, u64p, u64p, u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_extract_keys.argtypes = [P, u64p, C.POINTER(u64p), u64p, u64p, C.c_int64, u64p]
+        L.ref_sign_schedule.argtypes = [P, C.POINTER(C.c_int32), C.c_int32]; L.ref_sign_schedule.restype = C.c_int
         L.ref_sign_plan.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.ref_sign_precise_rounds.argtypes = [P]; L.ref_sign_precise_rounds.restype = C.c_int
         L.ref_bsk2_words.argtypes = [P, C.c_int]; L.ref_bsk2_words.restype = C.c_size_t
@@ -109,17 +113,16 @@ class RefTFHE:
         self.ksk = np.zeros(L.ref_ksk_words(C.byref(self.P)), np.uint64)
         L.ref_keygen(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big), u64(self.bsk),
                      u64(self.ksk))
-        # the fast gadgets' bootstrapping keys (fhe_keygen generates them too)
-        self.bsk2 = self.bsk3 = None
-        for which, lv in ((1, "pbs_fast_level"), (2, "pbs_fast2_level")):
+        # the other gadgets' bootstrapping keys (fhe_keygen generates them
+        # too): keys[g] for g = 1..4 (fast, fast2, mid, mid2)
+        self.keys = {}
+        for which, lv in GADGET_LEVEL.items():
             if self.params[lv]:
                 b = np.zeros(L.ref_bsk2_words(C.byref(self.P), which), np.uint64)
                 L.ref_keygen_fast_bsk(C.byref(self.P), C.c_uint64(seed), which, u64(self.s_small), u64(self.s_big),
                                       u64(b))
-                if which == 1:
-                    self.bsk2 = b
-                else:
-                    self.bsk3 = b
+                self.keys[which] = b
+        self.bsk2, self.bsk3 = self.keys.get(1), self.keys.get(2)
 
     def with_msg_bits(self, P: int) -> "RefTFHE":
         self.params["msg_bits"] = int(P)
@@ -211,12 +214,13 @@ class RefTFHE:
         return out
 
     def pbs_gadget(self, small: np.ndarray, gadget: int, tv: int) -> np.ndarray:
-        """pbs_const on gadget 0 (main), 1 (fast) or 2 (fast2), classic or
-        multi-bit by that gadget's group (fhe_pbs_gadget_batch)."""
+        """pbs_const on gadget 0 (main), 1 (fast), 2 (fast2), 3 (mid) or 4
+        (mid2), classic or multi-bit by that gadget's group
+        (fhe_pbs_gadget_batch)."""
         small = np.ascontiguousarray(small, dtype=np.uint64)
         cnt = small.size // (self.n + 1)
         out = np.zeros((cnt, self.big + 1), np.uint64)
-        key = self.bsk if gadget == 0 else self.bsk2 if gadget == 1 else self.bsk3
+        key = self.bsk if gadget == 0 else self.keys[gadget]
         lib().ref_pbs_gadget(C.byref(self.P), u64(key), u64(small), cnt, int(gadget), C.c_uint64(tv), u64(out))
         return out
 
@@ -252,9 +256,8 @@ class RefTFHE:
         cv = np.array(ct_v, dtype=np.uint64, copy=True, order="C")
         cnt = cv.size // (self.big + 1)
         sign = np.zeros((cnt, self.big + 1), np.uint64)
-        bsk2 = u64(self.bsk2) if self.bsk2 is not None else None
-        bsk3 = u64(self.bsk3) if self.bsk3 is not None else None
-        lib().ref_sign_extract3(C.byref(self.P), u64(self.bsk), bsk2, bsk3, u64(self.ksk), u64(cv), cnt, u64(sign))
+        keys = (C.POINTER(C.c_uint64) * 4)(*[u64(self.keys[g]) if g in self.keys else None for g in range(1, 5)])
+        lib().ref_sign_extract_keys(C.byref(self.P), u64(self.bsk), keys, u64(self.ksk), u64(cv), cnt, u64(sign))
         return sign
 
     def bit_extract(self, ct_v: np.ndarray):
@@ -318,3 +321,11 @@ def sign_plan(params: dict):
     d, j1, j2 = C.c_int32(), C.c_int32(), C.c_int32()
     lib().ref_sign_plan(C.byref(_ref_params(params)), C.byref(d), C.byref(j1), C.byref(j2))
     return d.value, j1.value, j2.value
+
+
+def sign_schedule(params: dict) -> list:
+    """The gadget (0 main, 1 fast, 2 fast2, 3 mid, 4 mid2) of every bootstrap
+    of the sign extraction (ref_sign_schedule)."""
+    out = (C.c_int32 * 64)()
+    R = lib().ref_sign_schedule(C.byref(_ref_params(params)), out, 64)
+    return [int(out[r]) for r in range(R)]

@@ -109,11 +109,47 @@ def test_build_info_and_kernel_names_on_host_context():
     h = C.c_void_p()
     assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
     buf = C.create_string_buffer(64)
-    for k in (b"blind_rotate", b"blind_rotate_main", b"blind_rotate_fast", b"blind_rotate_fast2", b"keyswitch"):
+    for k in (b"blind_rotate", b"blind_rotate_main", b"blind_rotate_fast", b"blind_rotate_fast2",
+              b"blind_rotate_mid", b"blind_rotate_mid2", b"keyswitch"):
         assert L.fhe_profile_kernel_name(h, k, buf, 64) == 0 and buf.value == b""
     assert L.fhe_profile_kernel_name(h, b"nope", buf, 64) == -1
     assert L.fhe_profile_kernel_name(h, b"keyswitch", None, 64) == -1
     assert L.fhe_pbs_table_batch(h, None, 0, None, 4, None, None) == -2
     assert L.fhe_threshold_batch(h, None, 0, 0, None, None) == -2
     assert L.fhe_debug_v4_stamps(h, buf) == -2
+    L.fhe_ctx_destroy(h)
+
+
+def test_mid_gadget_validation_and_schedule(oracle_lib):
+    """The mid-gadget fields: each pair all-or-nothing, mid needs the fast
+    gadget, mid2 needs mid; fhe_sign_schedule fills at most cap entries and
+    returns R; the mid keys' sizes (which = 3, 4) equal the oracle's."""
+    from fheicp.params import sign_schedule
+    L = _lib.lib()
+    h = C.c_void_p()
+    base = params_for_bits(26).as_dict()
+    assert base["pbs_mid_level"] and base["pbs_mid2_level"]
+    for bad, why in ((dict(base, pbs_mid_level=0), b"mid pbs"),
+                     (dict(base, pbs_mid_base_log=0, pbs_mid_level=0), b"mid2"),
+                     (dict(base, pbs_mid2_base_log=0), b"mid2"),
+                     (dict(base, pbs_fast_base_log=0, pbs_fast_level=0, pbs_fast2_base_log=0, pbs_fast2_level=0),
+                      b"mid pbs")):
+        P = _lib.params_struct(bad)
+        assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1, bad
+        assert why in L.fhe_last_error(None), L.fhe_last_error(None)
+        assert L.fhe_sign_schedule(C.byref(P), None, 0) == -1
+    P = _lib.params_struct(base)
+    R = L.fhe_sign_schedule(C.byref(P), None, 0)
+    want = sign_schedule(params_for_bits(26))[1]
+    assert R == len(want) == 17
+    out = (C.c_int32 * 4)(-1, -1, -1, -1)
+    assert L.fhe_sign_schedule(C.byref(P), out, 3) == R and list(out) == want[:3] + [-1]
+    ol = oracle_lib.lib()
+    RP = oracle_lib.RefParams(**base)
+    for which in (1, 2, 3, 4):
+        assert L.fhe_fast_bsk_words(C.byref(P), which) == ol.ref_bsk2_words(C.byref(RP), which) > 0, which
+    assert L.fhe_fast_bsk_words(C.byref(P), 5) == 0
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
+    buf = (C.c_uint64 * 1)()
+    assert L.fhe_export_fast_bsk(h, 3, buf) == -2
     L.fhe_ctx_destroy(h)

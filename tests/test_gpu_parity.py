@@ -224,12 +224,13 @@ def test_sign_toy_all_values_vs_oracle(need_gpu, oracle_lib, P, dbits):
 TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_level=2)
 
 
-@pytest.mark.parametrize("P,grp", [(8, 1), (16, 2), (16, 1), (19, 2)])
+@pytest.mark.parametrize("P,grp", [(8, 1), (16, 2), (16, 1), (19, 2), (26, 2)])
 def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
     """Every bootstrapping key of a multi-gadget parameter set (toy (12,3)+(8,2);
-    real P=16: (15,2) + (15,2) + (23,1); P=19: (12,3) + (15,2) + (23,1)) is
-    bit-exact against the oracle's keygen, the fast gadgets' keys as
-    multi-bit keys (group 2: three GGSWs per pair) and as classic ones."""
+    real P=16: (15,2) + (15,2) + (23,1); P=19: (12,3) + (15,2) + (23,1); P=26:
+    (6,7) + mid (8,5) + mid2 (12,3) + (15,2) + (23,1)) is bit-exact against
+    the oracle's keygen, the fast gadgets' keys as multi-bit keys (group 2:
+    three GGSWs per pair) and as classic ones."""
     prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 12 else params_for_bits(P)
     if P >= 12:
         prm = replace(prm, pbs_fast_group=grp, pbs_fast2_group=grp)
@@ -241,6 +242,40 @@ def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
     assert np.array_equal(eng.export_fast_bsk(1), ref.bsk2)
     if prm.pbs_fast2_level:
         assert np.array_equal(eng.export_fast_bsk(2), ref.bsk3)
+    for which in (3, 4):
+        if which in ref.keys:
+            assert np.array_equal(eng.export_fast_bsk(which), ref.keys[which]), which
+    assert (3 in ref.keys) == (P == 26)
+    eng.close()
+
+
+@pytest.mark.parametrize("P,dbits,mid2", [(11, 4, None), (11, 3, (9, 2))])
+def test_sign_toy_mid_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits, mid2):
+    """Mid gadgets (toy main (12,3) -> mid (10,2) [-> mid2 (9,2)] -> fast
+    (8,2) -> fast2 (11,1)): the schedule puts rounds on every key, the mid keys
+    are bit-exact, every value keeps its sign and the phases track the
+    oracle's five-key restatement."""
+    from fheicp.params import sign_schedule
+    kw = dict(TOY_FAST3, pbs_mid_base_log=10, pbs_mid_level=2)
+    if mid2:
+        kw.update(pbs_mid2_base_log=mid2[0], pbs_mid2_level=mid2[1])
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=dbits, **kw)
+    assert set(sign_schedule(prm)[1]) == ({0, 1, 2, 3, 4} if mid2 else {0, 1, 2, 3})
+    eng = Engine(prm, 0)
+    eng.keygen(4324)
+    ref = oracle_lib.RefTFHE(prm.as_dict(), 4324)
+    for which in sorted(ref.keys):
+        assert np.array_equal(eng.export_fast_bsk(which), ref.keys[which]), which
+    v = np.arange(-(2 ** (P - 1)), 2 ** (P - 1), dtype=np.int64)
+    sign = eng.sign(eng.encrypt(v, seed=64))
+    assert np.array_equal(eng.decrypt_bits(sign).cpu().numpy(), (v < 0).astype(np.int64))
+    h = 2 ** (P - 1)
+    sel = np.array([0, 1, h - 1, h, h + 1, 2 * h - 1])
+    s_ref = ref.sign_extract(ref.encrypt_ints(v[sel], seed=64, id0=0))
+    assert np.array_equal(ref.decrypt_bits(s_ref), (v[sel] < 0).astype(np.int64))
+    # the last round is on the coarse (11,1) toy gadget (see the three-gadget test)
+    dph = signed(u64(eng.phase(sign[sel].contiguous())) - ref.phase(s_ref))
+    assert np.abs(dph).max() < 2 ** 61
     eng.close()
 
 
@@ -308,10 +343,11 @@ def test_sign_toy_three_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits):
 
 
 @pytest.mark.parametrize("P,dbits,fast", [(16, 0, True), (16, 3, True), (16, 0, "classic"), (19, 0, True),
-                                          (19, 0, False), (21, 0, True), (21, 0, False)])
+                                          (19, 0, False), (21, 0, True), (21, 0, False), (26, 0, True)])
 def test_sign_real_params(need_gpu, P, dbits, fast):
-    """Real parameters at the C2/C4 (P=16: 4-bit digits, and 3-bit forced)
-    and C3 (P=21: 3-bit) widths, with (fast; multi-bit fast gadgets) and
+    """Real parameters at the C2/C4 (P=16: 4-bit digits, and 3-bit forced),
+    C3 (P=21: 3-bit) and C5 (P=26: five gadgets with the mid ones) widths,
+    with (fast; multi-bit fast gadgets) and
     without the per-round fast gadgets, and with the fast gadgets on the
     classic rotation ("classic"), boundaries included."""
     prm = params_for_bits(P, fast=bool(fast))

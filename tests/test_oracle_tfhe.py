@@ -211,6 +211,39 @@ def test_sign_extract_three_gadgets(oracle_lib, P, d):
     assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
 
 
+@pytest.mark.parametrize("P,d,mid2", [(11, 4, None), (11, 3, (9, 2))])
+def test_sign_extract_mid_gadgets(oracle_lib, P, d, mid2):
+    """Mid gadgets between the main and the fast one on a toy
+    set whose schedule uses every key: main (12,3) -> mid (10,2) [-> mid2
+    (9,2)] -> fast (8,2) -> fast2 (11,1). The values keep their sign, and the
+    schedule matches the library's and params.py's."""
+    import ctypes as C
+    from dataclasses import replace
+    from fheicp import _lib
+    from fheicp.params import TOY, sign_schedule
+    kw = dict(TOY_FAST3, pbs_mid_base_log=10, pbs_mid_level=2)
+    if mid2:
+        kw.update(pbs_mid2_base_log=mid2[0], pbs_mid2_level=mid2[1])
+    prm = replace(TOY, msg_bits=P, sign_digit_bits=d, **kw)
+    dd, sched = sign_schedule(prm)
+    assert dd == d and set(sched) == ({0, 1, 2, 3, 4} if mid2 else {0, 1, 2, 3}), sched
+    assert oracle_lib.sign_schedule(prm.as_dict()) == sched
+    out = (C.c_int32 * 64)()
+    R = _lib.lib().fhe_sign_schedule(C.byref(_lib.params_struct(prm.as_dict())), out, 64)
+    assert list(out[:R]) == sched
+    r = oracle_lib.RefTFHE(prm.as_dict(), 4323)
+    assert sorted(r.keys) == ([1, 2, 3, 4] if mid2 else [1, 2, 3])
+    h = 2 ** (P - 1)
+    v = np.concatenate([[-h, -h + 1, -2, -1, 0, 1, h - 2, h - 1],
+                        np.random.default_rng(P + d).integers(-h, h, 120)]).astype(np.int64)
+    sign = r.sign_extract(r.encrypt_ints(v, seed=400 + P))
+    assert np.array_equal(r.decrypt_bits(sign), (v < 0).astype(np.int64))
+    # each mid key is its own stream: a mid-gadget bootstrap on it keeps signs
+    small = r.keyswitch(r.encrypt_ints(np.array([-5, 7], np.int64) << (P - 4), seed=5))
+    ph = r.phase(r.pbs_gadget(small, 3, 1 << 61)).view(np.int64)
+    assert list(ph > 0) == [False, True]
+
+
 def test_multibit_rotation_oracle(oracle_lib):
     """The multi-bit blind rotation (group 2) in the oracle:
     an odd n (the last pair has a phantom zero coefficient), the key holds

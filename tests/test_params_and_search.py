@@ -9,7 +9,7 @@ import torch
 import torch.multiprocessing as mp
 
 from fheicp.params import (PBS_GADGETS, TOY, params_for_bits, noise_report, sign_digit_bits, sign_pbs_count,
-                           sign_plan, sign_precise_rounds, sign_rounds)
+                           sign_plan, sign_precise_rounds, sign_rounds, sign_schedule)
 from fheicp.search import sharded_topk
 
 
@@ -59,6 +59,9 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
         dd, j1, j2 = C.c_int32(), C.c_int32(), C.c_int32()
         assert L.fhe_sign_plan(cp, C.byref(dd), C.byref(j1), C.byref(j2)) == 0
         assert sign_plan(p) == oracle_lib.sign_plan(d) == (dd.value, j1.value, j2.value), d
+        sched = (C.c_int32 * 64)()
+        R = L.fhe_sign_schedule(cp, sched, 64)
+        assert sign_schedule(p)[1] == oracle_lib.sign_schedule(d) == list(sched[:R]), d
     # the headline width: 4-bit digits at P = 16, 3-bit where 4 misses the bar
     assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 3, 3, 3]
     assert sign_pbs_count(16) == 7
@@ -72,14 +75,13 @@ def test_fast_gadget_plan():
     rounds, whose output is shifted up the most, stay on the precise gadget,
     and every round keeps 9.2 sigma with the fewest main, then fast, rounds."""
     from fheicp.params import _plan_worst, plan_cost
-    F, Fc, F2 = (15, 2, 2), (15, 2, 1), (23, 1, 2)
+    F, F2 = (15, 2, 2), (23, 1, 2)
     want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F, F2, (4, 0, 1)), 12: (F, F2, (4, 0, 1)),
             13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 1, 3)), 17: (F, F2, (3, 0, 5)), 18: (F, F2, (4, 1, 5)),
-            19: (F, F2, (4, 1, 5)), 20: (Fc, F2, (4, 2, 5)), 21: (F, F2, (3, 3, 7)), 22: (F, F2, (3, 3, 9)),
-            23: (F, F2, (3, 4, 9)), 24: (F, F2, (3, 5, 9)), 25: (F, F2, (3, 5, 11)), 26: (F, F2, (3, 6, 11)),
-            27: (F, F2, (3, 7, 11))}
+            19: (F, F2, (4, 1, 5)), 21: (F, F2, (3, 3, 7))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
+        assert p.pbs_mid_level == 0, P
         assert (p.pbs_fast_base_log, p.pbs_fast_level, p.pbs_fast_group) == fg, P
         got2 = (p.pbs_fast2_base_log, p.pbs_fast2_level, p.pbs_fast2_group) if p.pbs_fast2_level else None
         assert got2 == fg2, P
@@ -95,6 +97,38 @@ def test_fast_gadget_plan():
     assert sign_plan(params_for_bits(16)) == (4, 1, 3)
     assert sign_plan(params_for_bits(19, fast=False)) == (4, 9, 9)
     assert params_for_bits(3).pbs_fast_level == 0
+
+
+def test_mid_gadget_plan():
+    """Mid gadgets: at P = 20 and from P = 22 the plan adds one or two
+    cheaper main gadgets between the main and the fast one. The schedule walks
+    main -> mid -> mid2 -> fast -> fast2, each gadget on the fewest rounds for
+    which the next one on all the rest keeps every decision at 9.2 sigma, and
+    the plan is cheaper than the same gadgets without mids."""
+    from dataclasses import replace
+    from fheicp.params import _sched_worst, plan_cost, sign_schedule
+    want = {20: ((15, 2), None), 22: ((12, 3), None), 23: ((12, 3), None), 24: ((10, 4), (12, 3)), 25: ((10, 4), (12, 3)),
+            26: ((8, 5), (12, 3)), 27: ((8, 5), (12, 3))}
+    for P, (m1, m2) in want.items():
+        p = params_for_bits(P)
+        assert (p.pbs_mid_base_log, p.pbs_mid_level) == m1, P
+        assert ((p.pbs_mid2_base_log, p.pbs_mid2_level) if p.pbs_mid2_level else None) == m2, P
+        d, sched = sign_schedule(p)
+        assert len(sched) == sign_pbs_count(p) and _sched_worst(p, d, sched) >= 9.2, P
+        lad = [g for g in (0, 3, 4, 1, 2) if g in sched]
+        assert sched == sorted(sched, key=lad.index), P   # ladder order
+        for i in range(len(lad) - 1):                      # each gadget on its fewest rounds
+            c = sched.index(lad[i + 1])
+            start = sched.index(lad[i])
+            if c > start:
+                fewer = sched[:c - 1] + [lad[i + 1]] * (len(sched) - c + 1)
+                assert _sched_worst(p, d, fewer) < 9.2, (P, i)
+        nomid = replace(p, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid2_base_log=0, pbs_mid2_level=0)
+        assert plan_cost(p) < plan_cost(nomid), P
+    # C5's width: 1 main (6,7), 2 mid (8,5), 3 mid2 (12,3), 5 fast, 6 fast2
+    assert sign_schedule(params_for_bits(26))[1] == [0, 3, 3, 4, 4, 4] + [1] * 5 + [2] * 6
+    # the headline and C3 widths have no mid gadget
+    assert params_for_bits(16).pbs_mid_level == 0 and params_for_bits(21).pbs_mid_level == 0
 
 
 def test_multibit_noise_model():
