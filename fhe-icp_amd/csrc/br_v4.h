@@ -348,7 +348,14 @@ struct Acc<true> {
     return (T)(uint32_t)__builtin_bit_cast(uint64_t, t35) << 3;
 #endif
     const double f = __builtin_amdgcn_fract(z);
+#ifdef FHEICP_FMA_ROUND
     const double t = __fma_rn(f, 4294967296.0, 6755399441055744.0);
+#else
+    // f * 2^32 is exact, so the add rounds once as the fma would; the fma's
+    // accumulator operand costs two v_mov per coefficient (its destination
+    // is the 1.5 * 2^52 constant), ldexp + add with an SGPR constant none
+    const double t = __builtin_ldexp(f, 32) + 6755399441055744.0;
+#endif
     return (T)(uint32_t)__builtin_bit_cast(uint64_t, t);
   }
 };

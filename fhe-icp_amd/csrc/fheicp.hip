@@ -978,26 +978,33 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   } else if (fast && mb_for(ctx->p, gad)) {
     // multi-bit rotation, key-stationary products (k_blind_rotate_mb)
     const dim3 gm((unsigned)((count + 3) / 4)), bm(v4::nthreads(4));
-#define MBD(L, D)                                                                                               \
-  hipLaunchKernelGGL((k_blind_rotate_mb<L, D>), gm, bm, 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, \
+#define MBD(L, D, B)                                                                                            \
+  hipLaunchKernelGGL((k_blind_rotate_mb<L, D, B>), gm, bm, 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, \
                      ctx->tw4, ctx->psi, tv, mode, out, ct_v, refreshed, sign)
 #ifdef FHEICP_AB
     if (ctx->mb_dbg) {
       const int w = ctx->mb_dbg >> 8;
-      if (ctx->mb_dbg == 2) { if (p.pbs_level == 1) MBD(1, 2); else MBD(2, 2); }
-      else if (ctx->mb_dbg == 130) { if (p.pbs_level == 1) MBD(1, 130); else MBD(2, 130); }
-      else if (w == 0) { if (p.pbs_level == 1) MBD(1, 128); else MBD(2, 128); }
-      else if (w == 1) { if (p.pbs_level == 1) MBD(1, 128 + 256); else MBD(2, 128 + 256); }
-      else { if (p.pbs_level == 1) MBD(1, 128 + 512); else MBD(2, 128 + 512); }
+      if (ctx->mb_dbg == 2) { if (p.pbs_level == 1) MBD(1, 2, 0); else MBD(2, 2, 0); }
+      else if (ctx->mb_dbg == 130) { if (p.pbs_level == 1) MBD(1, 130, 0); else MBD(2, 130, 0); }
+      else if (w == 0) { if (p.pbs_level == 1) MBD(1, 128, 0); else MBD(2, 128, 0); }
+      else if (w == 1) { if (p.pbs_level == 1) MBD(1, 128 + 256, 0); else MBD(2, 128 + 256, 0); }
+      else { if (p.pbs_level == 1) MBD(1, 128 + 512, 0); else MBD(2, 128 + 512, 0); }
       name = "k_blind_rotate_mb<DBG>";
     } else
 #endif
-    if (p.pbs_level == 1) {
-      MBD(1, 0);
-      name = "k_blind_rotate_mb<1, 0>";
+    // the shipped fast gadgets (23,1) and (15,2) with their base log fixed
+    if (p.pbs_level == 1 && p.pbs_base_log == 23) {
+      MBD(1, 0, 23);
+      name = "k_blind_rotate_mb<1, 0, 23>";
+    } else if (p.pbs_level == 1) {
+      MBD(1, 0, 0);
+      name = "k_blind_rotate_mb<1, 0, 0>";
+    } else if (p.pbs_base_log == 15) {
+      MBD(2, 0, 15);
+      name = "k_blind_rotate_mb<2, 0, 15>";
     } else {
-      MBD(2, 0);
-      name = "k_blind_rotate_mb<2, 0>";
+      MBD(2, 0, 0);
+      name = "k_blind_rotate_mb<2, 0, 0>";
     }
 #undef MBD
   } else if (p.N == 1024 && p.k == 2 && var == 4 && !v4_a32(ctx, p)) {

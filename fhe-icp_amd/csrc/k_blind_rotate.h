@@ -648,8 +648,12 @@ __host__ __device__ constexpr int psi_pos(int x) { return x ^ ((x >> 4) & 15); }
 //   quarter -> barrier] x L -> products to the owners' slots -> barrier ->
 //   own slot -> inverse
 // DBG != 0 only in A/B timing builds: 2 = no key loads (wrong results), 128 =
-// phase timestamps of wave DBG >> 8 of workgroup 0, pairs 100..103
-template <int L, int DBG = 0>
+// phase timestamps of wave DBG >> 8 of workgroup 0, pairs 100..103.
+// BETA != 0: the gadget base log as a constant (the shipped fast gadgets),
+// which folds the digit shifts and widths into inline operands; 0 = `beta`.
+// Key rows come through buffer loads: a per-lane offset fixed for the kernel
+// and a scalar offset per row, so the loads take no VALU address arithmetic.
+template <int L, int DBG = 0, int BETA = 0>
 __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u64* __restrict__ small, int64_t count, int n,
                                                                       int beta, const c64* __restrict__ bsk,
                                                                       const c64* __restrict__ tw4,
@@ -673,6 +677,9 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
   c64* slot = xbuf + (g * WPC + comp) * SCR;
   T* sa = reinterpret_cast<T*>(slot);
   const int np = (n + 1) >> 1;
+  const int bta = BETA ? BETA : beta;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)bsk, (short)0, 0x7fffffff, 0x00020000);
+  const int kvoff = (comp * M + 2 * g * 64 + lane) * (int)sizeof(c64);
 
   fill_tables(twl, tw4, tid, NT);
   for (int x = tid; x < NPSI; x += NT) psil[x] = psi[x];
@@ -720,7 +727,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
     for (int s = 0; s < S; ++s) {
       int d[2][L];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) decompose_v4<L, true>(acc[s + h * S], beta, d[h]);
+      for (int h = 0; h < 2; ++h) decompose_v4<L, true>(acc[s + h * S], bta, d[h]);
       v[s] = {(double)d[0][0], (double)d[1][0]};
 #pragma unroll
       for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
@@ -729,7 +736,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
     c64 o[G][2];  // products of the quarter, per ciphertext
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
-    const c64* Gj = bsk + (size_t)j * 3 * R * WPC * M + (size_t)comp * M + 2 * g * 64 + lane;
+    const int kjoff = j * 3 * R * WPC * M * (int)sizeof(c64);  // this pair's key, bytes
 #pragma unroll
     for (int lv = 0; lv < L; ++lv) {
       if (lv > 0) {
@@ -745,7 +752,8 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
 #pragma unroll
           for (int r = 0; r < WPC; ++r)
             k[Ss][r] = (DBG & 2) ? c64{0.25 + r, 0.5 * t + Ss}
-                                 : Gj[((size_t)(Ss * R + r * L + lv) * WPC) * M + t * 64];
+                                 : __builtin_bit_cast(c64, __builtin_amdgcn_raw_buffer_load_b128(
+                                       krs, kvoff, kjoff + (((Ss * R + r * L + lv) * WPC) * M + t * 64) * (int)sizeof(c64), 0));
       };
       // (loading the first slot's rows before the transform instead, at L = 1:
       // 4.06 vs 4.04 ms per 1024, not kept)

@@ -7,7 +7,7 @@ DESIGN.md §3.5). Sampling a thousand compares cannot show that, so for each
 kernel instance the parameter table can select (v4 32-bit accumulators at
 (15,2) and (23,1), the key-stationary v4s with 64-bit accumulators at (12,3),
 v2 at levels 4..8, and the multi-bit rotation of the fast gadgets at (15,2)
-and (23,1)) this measures the output noise of >= 4096 bootstraps on the real
+and (23,1), plus its run-time-base-log instances) this measures the output noise of >= 4096 bootstraps on the real
 parameters and checks it against the model (fheicp.params._variances, the
 same formula as fheicp.hip and oracle/tfhe_ref.c), and checks a few output
 phases against the exact oracle's bootstrap of the same inputs.
@@ -35,8 +35,11 @@ INSTANCES = {
     (7, 6, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
     (6, 7, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
     (5, 8, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (15, 2, 2): "k_blind_rotate_mb<2, 0>",
-    (23, 1, 2): "k_blind_rotate_mb<1, 0>",
+    (15, 2, 2): "k_blind_rotate_mb<2, 0, 15>",
+    (23, 1, 2): "k_blind_rotate_mb<1, 0, 23>",
+    # the multi-bit kernels with a run-time base log (other gadgets)
+    (14, 2, 2): "k_blind_rotate_mb<2, 0, 0>",
+    (22, 1, 2): "k_blind_rotate_mb<1, 0, 0>",
 }
 COUNT = 4096
 TV = 1 << 61
