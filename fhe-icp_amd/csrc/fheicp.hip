@@ -886,7 +886,7 @@ static bool launch_br_ab(fhe_ctx* ctx, const fhe_params& p, const uint64_t* d_sm
                          uint64_t* ct_v, uint64_t* refreshed, uint64_t* sign, const c64* bsk_fft, hipStream_t st,
                          const char** name) {
   const bool a32 = v4_a32(ctx, p);
-#define AB4(L, A32, D, GG, FLAGS)                                                                               do {                                                                                                            hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),                           dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft,                               ctx->tw4, tv, mode, out, ct_v, refreshed, sign);                                           *name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ">";                                    return true;                                                                                                } while (0)
+#define AB4(L, A32, D, GG, FLAGS)                                                                               do {                                                                                                            hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),                           dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft,                               ctx->tw4, tv, mode, out, ct_v, refreshed, sign);                                           *name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ", 0>";                                    return true;                                                                                                } while (0)
 #define AB4G(L, A32, D, GG)   do { if (ctx->v4_fl && GG > 1) AB4(L, A32, D, GG, true); else AB4(L, A32, D, GG, false); } while (0)
 #define AB4D(D)   do { if (ctx->v4_g == 1) AB4G(2, true, D, 1); else if (ctx->v4_g == 2) AB4G(2, true, D, 2); else AB4G(2, true, D, 4); } while (0)
   if (ctx->v4_dbg && p.pbs_level == 2 && a32) {
@@ -954,12 +954,12 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
                        p.pbs_base_log, bsk_fft, ctx->tw, ctx->twist, tv, mode, out, ct_v, refreshed, sign);   \
     name = "k_blind_rotate_mw<fhei::" #V ", " #K ", " #W ", BrTv>";                                           \
   } while (0)
-#define BR4F(L, A32, D, GG, FLAGS)                                                                            \
+#define BR4F(L, A32, D, GG, FLAGS, B)                                                                         \
   do {                                                                                                        \
-    hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS>), dim3((unsigned)((count + GG - 1) / GG)),    \
+    hipLaunchKernelGGL((k_blind_rotate_v4<L, A32, D, GG, FLAGS, B>), dim3((unsigned)((count + GG - 1) / GG)), \
                        dim3(v4::nthreads(GG)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, \
                        tv, mode, out, ct_v, refreshed, sign);                                                 \
-    name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ">";                                 \
+    name = "k_blind_rotate_v4<" #L ", " #A32 ", " #D ", " #GG ", " #FLAGS ", " #B ">";                         \
   } while (0)
   // The shipped N = 1024, k = 2 instances: the multi-bit kernels for fast
   // gadgets with pbs_fast*_group = 2; v4 at 4 ciphertexts per workgroup (3
@@ -1010,24 +1010,34 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
   } else if (p.N == 1024 && p.k == 2 && var == 4 && !v4_a32(ctx, p)) {
     // 64-bit accumulators: the key-stationary v4s kernels, 4 ciphertexts per
     // workgroup (15.9 vs 20.7 ms per 1024 at (12,3) for v4 at 2 per workgroup)
-#define BR4S(L)                                                                                               \
+#define BR4S(L, B)                                                                                            \
   do {                                                                                                        \
-    hipLaunchKernelGGL((k_blind_rotate_v4s<L, false>), dim3((unsigned)((count + 3) / 4)), dim3(v4::nthreads(4)), \
-                       0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4, tv, mode, out, ct_v,    \
-                       refreshed, sign);                                                                      \
-    name = "k_blind_rotate_v4s<" #L ", false, 0>";                                                             \
+    hipLaunchKernelGGL((k_blind_rotate_v4s<L, false, 0, B>), dim3((unsigned)((count + 3) / 4)),              \
+                       dim3(v4::nthreads(4)), 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft, ctx->tw4,  \
+                       tv, mode, out, ct_v, refreshed, sign);                                                 \
+    name = "k_blind_rotate_v4s<" #L ", false, 0, " #B ">";                                                     \
   } while (0)
+    // run-time base log: fixing (12, 3)'s at compile time made the compiler
+    // emit 144 more f64 instructions per step and a 56-byte spill
     switch (p.pbs_level) {
-      case 1: BR4S(1); break;
-      case 2: BR4S(2); break;
-      case 3: BR4S(3); break;
+      case 1: BR4S(1, 0); break;
+      case 2: BR4S(2, 0); break;
+      case 3: BR4S(3, 0); break;
       default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: pbs_level > 3");
     }
 #undef BR4S
   } else if (p.N == 1024 && p.k == 2 && var == 4) {
     switch (p.pbs_level) {
-      case 1: BR4F(1, true, 0, 4, false); break;
-      case 2: BR4F(2, true, 0, 4, false); break;
+      // (23, 1) and (15, 2), the classic gadgets of the parameter table, with
+      // their base log fixed; others on the run-time instances
+      case 1:
+        if (p.pbs_base_log == 23) BR4F(1, true, 0, 4, false, 23);
+        else BR4F(1, true, 0, 4, false, 0);
+        break;
+      case 2:
+        if (p.pbs_base_log == 15) BR4F(2, true, 0, 4, false, 15);
+        else BR4F(2, true, 0, 4, false, 0);
+        break;
       default: return fail(ctx, FHE_E_ARG, "v4 blind rotation: 32-bit accumulators need pbs_level <= 2");
     }
   } else if (p.N == 256 && p.k == 1) BR(7, 1);

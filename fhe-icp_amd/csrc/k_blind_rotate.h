@@ -363,7 +363,7 @@ __device__ unsigned long long g_v4_span[2048][3];
 // relayout, 16 no LDS rotation, 32 no LDS reads of the other components,
 // 128 phase timestamps (results correct).
 constexpr int FL_SYNC = 1;
-template <int L, bool A32, int DBG = 0, int G = 2, bool FL = false>
+template <int L, bool A32, int DBG = 0, int G = 2, bool FL = false, int BETA = 0>
 __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
                                                               const c64* __restrict__ tw4, BrTv tv, int mode,
@@ -414,6 +414,15 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
 
   constexpr int R = WPC * L;
   const c64 wf = {0.5 + (double)beta * 1e-3, (double)L * 1e-3};  // DBG stand-in value
+  // BSK rows through buffer loads: the lane's offset is fixed, the row's
+  // (uniform: step, level, components) goes in the scalar offset; BETA != 0
+  // fixes the base log at compile time (the shipped gadgets)
+  const int bta = BETA ? BETA : beta;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)bsk, (short)0, 0x7fffffff, 0x00020000);
+  const int klane = lane * (int)sizeof(c64);
+  auto krow = [&](int row_c64, int u) -> c64 {  // element u * 64 + lane of the row at row_c64
+    return __builtin_bit_cast(c64, __builtin_amdgcn_raw_buffer_load_b128(krs, klane, (row_c64 + u * 64) * (int)sizeof(c64), 0));
+  };
   for (int i = 0; i < n; ++i) {
     // FL: per-ciphertext hand-offs within a step, but one workgroup barrier
     // every FL_SYNC steps bounds how far the oldest ciphertext (highest issue
@@ -445,7 +454,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       for (int h = 0; h < 2; ++h) {
         const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
         const T r = src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S];
-        decompose_v4<L, A32>((T)(r - acc[s + h * S]), beta, d[h]);
+        decompose_v4<L, A32>((T)(r - acc[s + h * S]), bta, d[h]);
       }
       v[s] = {(double)d[0][0], (double)d[1][0]};
 #pragma unroll
@@ -456,7 +465,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
     c64 mac[S];
 #pragma unroll
     for (int u = 0; u < S; ++u) mac[u] = {0.0, 0.0};
-    const c64* Gi = bsk + (size_t)i * R * WPC * M;
+    const int Gi = i * R * WPC * M;  // this step's GGSW, in c64 from bsk
 #pragma unroll
     for (int lv = 0; lv < L; ++lv) {
       if (lv > 0) {
@@ -467,11 +476,11 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       // own-component BSK row: loads fly during the transform (which folds
       // the twist in); the u64 kernels load it after the transform (VGPRs)
       constexpr bool PF = A32 || G <= 2;  // u64 kernels at 4 per workgroup: load late (VGPRs)
-      const c64* gpo = Gi + ((size_t)(comp * L + lv) * WPC + comp) * M;
+      const int gpo = Gi + ((comp * L + lv) * WPC + comp) * M;
       c64 kb[PF ? S : 1];
       if constexpr (PF) {
 #pragma unroll
-        for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : gpo[u * 64 + lane];
+        for (int u = 0; u < S; ++u) kb[u] = (DBG & 2) ? c64{wf.x + u, wf.y} : krow(gpo, u);
       }
       // the 32-bit-accumulator kernels also start one of the two other rows'
       // loads before the transform, at the first level (the MAC accumulator
@@ -483,9 +492,9 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       c64 ke[EARLY_CT ? S : 1];
       if (EARLY_CT && EARLY) {
         const int cin = comp + 1 >= WPC ? comp + 1 - WPC : comp + 1;
-        const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
+        const int gp = Gi + ((cin * L + lv) * WPC + comp) * M;
 #pragma unroll
-        for (int u = 0; u < S; ++u) ke[u] = (DBG & 2) ? c64{wf.x, wf.y + u} : gp[u * 64 + lane];
+        for (int u = 0; u < S; ++u) ke[u] = (DBG & 2) ? c64{wf.x, wf.y + u} : krow(gp, u);
       }
       // FL: the others must have read this slot's previous F before the
       // transform's relayouts overwrite it
@@ -500,7 +509,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
 #pragma unroll
       for (int u = 0; u < S; ++u) {
         if constexpr (PF) cmac(mac[u], v[u], kb[u]);
-        else cmac(mac[u], v[u], (DBG & 2) ? c64{wf.x + u, wf.y} : gpo[u * 64 + lane]);
+        else cmac(mac[u], v[u], (DBG & 2) ? c64{wf.x + u, wf.y} : krow(gpo, u));
       }
       // the other two rows' BSK: A32 kernels issue the loads before the
       // barrier (they fly across it); the u64-accumulator kernels load them
@@ -511,11 +520,11 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
 #pragma unroll
         for (int ci = 0; ci < K; ++ci) {
           const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
-          const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
+          const int gp = Gi + ((cin * L + lv) * WPC + comp) * M;
 #pragma unroll
           for (int u = 0; u < S; ++u) {
             if (EARLY && ci == 0) kx[ci][u] = ke[u];
-            else kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[u * 64 + lane];
+            else kx[ci][u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : krow(gp, u);
           }
         }
       }
@@ -533,7 +542,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       for (int ci = 0; ci < K; ++ci) {
         const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
         const c64* fs = ctslots + cin * SCR;
-        const c64* gp = Gi + ((size_t)(cin * L + lv) * WPC + comp) * M;
+        const int gp = Gi + ((cin * L + lv) * WPC + comp) * M;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {  // F in halves: bounds register use at the peak
           c64 fv[S / 2], kv[S / 2];
@@ -541,7 +550,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
           for (int u = 0; u < S / 2; ++u) {
             fv[u] = (DBG & 32) ? v[hh * 4 + u] : fs[(hh * 4 + u) * 64 + lane];
             if constexpr (PF) kv[u] = kx[ci][hh * 4 + u];
-            else kv[u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : gp[(hh * 4 + u) * 64 + lane];
+            else kv[u] = (DBG & 2) ? c64{wf.x + ci, wf.y + u} : krow(gp, hh * 4 + u);
           }
 #pragma unroll
           for (int u = 0; u < S / 2; ++u) cmac(mac[hh * 4 + u], fv[u], kv[u]);
@@ -850,8 +859,10 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
 // k_blind_rotate_mb: wave (g, c) forms output component c of all four
 // ciphertexts on the slot quarter {2g, 2g+1}, so each key element is loaded
 // once per CU (6 loads per wave and level instead of 24) and goes back to the
-// owner through LDS (2L + 1 barriers per step instead of 2L).
-template <int L, bool A32, int DBG = 0>
+// owner through LDS (2L + 1 barriers per step instead of 2L). Key rows come
+// through buffer loads (scalar row offsets) and BETA != 0 fixes the base log
+// at compile time, as in k_blind_rotate_mb.
+template <int L, bool A32, int DBG = 0, int BETA = 0>
 __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u64* __restrict__ small, int64_t count, int n,
                                                                       int beta, const c64* __restrict__ bsk,
                                                                       const c64* __restrict__ tw4, BrTv tv, int mode,
@@ -890,15 +901,20 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
   }
 
   constexpr int R = WPC * L;
-  // this wave's key column and slot quarter
-  const c64* Gc = bsk + (size_t)comp * M + 2 * g * 64 + lane;
+  const int bta = BETA ? BETA : beta;
+  // this wave's key column and slot quarter: a per-lane offset fixed for the
+  // kernel, a scalar one per row
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)bsk, (short)0, 0x7fffffff, 0x00020000);
+  const int kvoff = (comp * M + 2 * g * 64 + lane) * (int)sizeof(c64);
   auto load = [&](int i, int lv, c64 (&k)[2][WPC]) {
-    const c64* Gi = Gc + (size_t)i * R * WPC * M;
+    const int ki = i * R * WPC * M * (int)sizeof(c64);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < WPC; ++r)
-        k[t][r] = (DBG & 2) ? c64{0.25 + r, 0.5 * t + lv} : Gi[((size_t)(r * L + lv) * WPC) * M + t * 64];
+        k[t][r] = (DBG & 2) ? c64{0.25 + r, 0.5 * t + lv}
+                            : __builtin_bit_cast(c64, __builtin_amdgcn_raw_buffer_load_b128(
+                                  krs, kvoff, ki + (((r * L + lv) * WPC) * M + t * 64) * (int)sizeof(c64), 0));
   };
   static_assert(L <= WPC, "key buffers per level");
   c64 kb[L][2][WPC];  // [level][slot t][row]
@@ -926,7 +942,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       for (int h = 0; h < 2; ++h) {
         const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
         const T r = src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S];
-        decompose_v4<L, A32>((T)(r - acc[s + h * S]), beta, d[h]);
+        decompose_v4<L, A32>((T)(r - acc[s + h * S]), bta, d[h]);
       }
       v[s] = {(double)d[0][0], (double)d[1][0]};
 #pragma unroll

@@ -27,9 +27,11 @@ pytestmark = pytest.mark.gpu
 # (base_log, level, group) -> the instantiation fhe_profile_kernel_name
 # reports; group 2 = the multi-bit rotation, run as a fast gadget
 INSTANCES = {
-    (15, 2, 1): "k_blind_rotate_v4<2, true, 0, 4, false>",
-    (23, 1, 1): "k_blind_rotate_v4<1, true, 0, 4, false>",
-    (12, 3, 1): "k_blind_rotate_v4s<3, false, 0>",
+    (15, 2, 1): "k_blind_rotate_v4<2, true, 0, 4, false, 15>",
+    (23, 1, 1): "k_blind_rotate_v4<1, true, 0, 4, false, 23>",
+    (14, 2, 1): "k_blind_rotate_v4<2, true, 0, 4, false, 0>",   # run-time base log
+    (22, 1, 1): "k_blind_rotate_v4<1, true, 0, 4, false, 0>",
+    (12, 3, 1): "k_blind_rotate_v4s<3, false, 0, 0>",
     (10, 4, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
     (8, 5, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
     (7, 6, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
