@@ -916,11 +916,22 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
                             : __builtin_bit_cast(c64, __builtin_amdgcn_raw_buffer_load_b128(
                                   krs, kvoff, ki + (((r * L + lv) * WPC) * M + t * 64) * (int)sizeof(c64), 0));
   };
-  static_assert(L <= WPC, "key buffers per level");
-  c64 kb[L][2][WPC];  // [level][slot t][row]
-#ifdef FHEICP_V4S_EARLY
-  load(0, 0, kb[0]);
-#endif
+  // From L = 3 the level loop stays rolled: unrolled, the compiler hoists
+  // work across levels and spills (28 bytes at L = 3, 172-532 at L = 4-7;
+  // rolled: 0 at L = 3). From L = 4 the digits are not kept per level but
+  // re-extracted from the rounded difference plus the balancing offset
+  // sum_i (B/2) B^i: digit_i = ((r' >> i beta) & (B - 1)) - B/2 equals the
+  // sequential balanced decomposition (the same representation mod B^L).
+  constexpr bool ROLL = L >= 3;
+  constexpr bool RECOMP = L >= 4;
+  static_assert(!RECOMP || !A32, "re-extracted digits are for the 64-bit accumulators");
+  u64 coff = 0;
+  if constexpr (RECOMP)
+    for (int l = 0; l < L; ++l) coff += (u64)1 << (l * bta + bta - 1);
+  auto digit_at = [&](u64 rr, int lv) -> double {
+    return (double)((int)((rr >> ((L - 1 - lv) * bta)) & ((1u << bta) - 1u)) - (1 << (bta - 1)));
+  };
+  c64 kb[2][WPC];  // this level's rows: [slot t][row]
   for (int i = 0; i < n; ++i) {
     [[maybe_unused]] unsigned long long stamp_[16];
     V4_STAMP(0);
@@ -928,7 +939,8 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
 #pragma unroll
     for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];  // own slot: in-order DS, no wait
     c64 v[S];
-    uint32_t dg[L > 1 ? L - 1 : 1][S];
+    uint32_t dg[(L > 1 && !RECOMP) ? L - 1 : 1][S];
+    u64 rr[RECOMP ? 2 * S : 1];
     T rot[2 * S];
 #pragma unroll
     for (int s = 0; s < 2 * S; ++s) {
@@ -937,47 +949,53 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      int d[2][L];
+      if constexpr (RECOMP) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
-        const T r = src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S];
-        decompose_v4<L, A32>((T)(r - acc[s + h * S]), bta, d[h]);
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
+          const u64 x = (u64)((src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S]) - acc[s + h * S]);
+          rr[s + h * S] = (((x >> (63 - L * bta)) + 1) >> 1) + coff;
+        }
+        v[s] = {digit_at(rr[s], 0), digit_at(rr[s + S], 0)};
+      } else {
+        int d[2][L];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
+          const T r = src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S];
+          decompose_v4<L, A32>((T)(r - acc[s + h * S]), bta, d[h]);
+        }
+        v[s] = {(double)d[0][0], (double)d[1][0]};
+#pragma unroll
+        for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
       }
-      v[s] = {(double)d[0][0], (double)d[1][0]};
-#pragma unroll
-      for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
     }
     V4_STAMP(1);
     c64 o[G][2];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
-#pragma unroll
+    constexpr int UNROLL_LV = ROLL ? 1 : L;
+#pragma unroll UNROLL_LV
     for (int lv = 0; lv < L; ++lv) {
       if (lv > 0) {
 #pragma unroll
-        for (int u = 0; u < S; ++u)
-          v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+        for (int u = 0; u < S; ++u) {
+          if constexpr (RECOMP)
+            v[u] = {digit_at(rr[u], lv), digit_at(rr[u + S], lv)};
+          else
+            v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+        }
       }
-#ifdef FHEICP_V4S_PRE  // A/B: this level's rows fly during its transform
-      load(i, lv, kb[lv]);
-#endif
+      // (this level's rows loaded before the transform, or the next level's
+      // during the products, measured slower: FHEICP_V4S=1 A/B, round 2)
       forward(v, twl, slot, lane);
       V4_STAMP(2 + 4 * lv);
 #pragma unroll
       for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
-#if !defined(FHEICP_V4S_EARLY) && !defined(FHEICP_V4S_PRE)
-      load(i, lv, kb[lv]);
-#endif
+      load(i, lv, kb);
       V4_STAMP(3 + 4 * lv);
       lds_barrier();
       V4_STAMP(4 + 4 * lv);
-#ifdef FHEICP_V4S_EARLY
-      // the next level's (or the next step's first level's) key rows fly
-      // during these products and the next transform
-      if (lv + 1 < L) load(i, lv + 1, kb[lv + 1]);
-      else if (L > 1 && i + 1 < n) load(i + 1, 0, kb[0]);
-#endif
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int u = 2 * g + t;
@@ -987,15 +1005,12 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
 #pragma unroll
           for (int r = 0; r < WPC; ++r) F[r] = xbuf[(gg * WPC + r) * SCR + u * 64 + lane];
 #pragma unroll
-          for (int r = 0; r < WPC; ++r) cmac(o[gg][t], F[r], kb[lv][t][r]);
+          for (int r = 0; r < WPC; ++r) cmac(o[gg][t], F[r], kb[t][r]);
 #ifdef FHEICP_V4S_SB
           __builtin_amdgcn_sched_barrier(0);  // keep the F reads from all being hoisted (VGPRs)
 #endif
         }
       }
-#ifdef FHEICP_V4S_EARLY
-      if (L == 1 && i + 1 < n) load(i + 1, 0, kb[0]);  // after its last use
-#endif
       V4_STAMP(5 + 4 * lv);
       lds_barrier();
     }

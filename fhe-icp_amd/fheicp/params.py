@@ -71,14 +71,14 @@ SIGMA_BAR = 9.2
 # candidate fast gadgets for the low-amplification sign rounds, each with
 # the classic (1) or the multi-bit (2) blind rotation, and the blind-rotation
 # time per bootstrap by (level, group) relative to L = 2 classic, measured on
-# MI355X at 1024 ciphertexts (tools/prof_br.py --gadget, tools/lib_ab.sh):
-# classic v4 (32-bit accumulators) L = 1, 2: 6.0 / 9.85 ms; key-stationary
-# v4s (64-bit) L = 3: 15.7 ms; v2 L = 4..8: 29.0 / 34.5 / 40.2 / 45.8 / 51.5
-# ms (prof_br times, 10.9 ms at L = 2 classic); multi-bit L = 1, 2: 4.05 /
-# 6.78 ms. Only the ranking matters.
+# MI355X at 1024 ciphertexts (tools/prof_br.py --gadget, tools/deep_ab.sh,
+# tools/lib_ab.sh): classic v4 (32-bit accumulators) L = 1, 2: 6.0 / 9.45 ms;
+# key-stationary v4s (64-bit) L = 3..8: 16.0 / 19.6 / 23.0 / 26.4 / 29.5 /
+# 32.8 ms (prof_br times, 11.2 ms at L = 2 classic); multi-bit L = 1, 2:
+# 4.0 / 6.7 ms. Only the ranking matters.
 FAST_GADGETS = ((15, 2, 1), (23, 1, 1), (15, 2, 2), (23, 1, 2))
-BR_COST = {(1, 1): 0.61, (2, 1): 1.0, (3, 1): 1.43, (4, 1): 2.65, (5, 1): 3.16, (6, 1): 3.68, (7, 1): 4.19,
-           (8, 1): 4.71, (1, 2): 0.41, (2, 2): 0.69}
+BR_COST = {(1, 1): 0.61, (2, 1): 1.0, (3, 1): 1.43, (4, 1): 1.75, (5, 1): 2.05, (6, 1): 2.35, (7, 1): 2.63,
+           (8, 1): 2.92, (1, 2): 0.41, (2, 2): 0.69}
 
 
 def sign_rounds(P: int, d: int):

@@ -5,8 +5,8 @@ Every decision of the sign extraction is exact only while the noise stays
 inside its margin (>= 9.2 sigma of the model, p_fail <= 2^-64 per bootstrap;
 DESIGN.md §3.5). Sampling a thousand compares cannot show that, so for each
 kernel instance the parameter table can select (v4 32-bit accumulators at
-(15,2) and (23,1), the key-stationary v4s with 64-bit accumulators at (12,3),
-v2 at levels 4..8, and the multi-bit rotation of the fast gadgets at (15,2)
+(15,2) and (23,1), the key-stationary v4s with 64-bit accumulators at (12,3)
+and levels 4..8, and the multi-bit rotation of the fast gadgets at (15,2)
 and (23,1), plus its run-time-base-log instances) this measures the output noise of >= 4096 bootstraps on the real
 parameters and checks it against the model (fheicp.params._variances, the
 same formula as fheicp.hip and oracle/tfhe_ref.c), and checks a few output
@@ -32,11 +32,11 @@ INSTANCES = {
     (14, 2, 1): "k_blind_rotate_v4<2, true, 0, 4, false, 0>",   # run-time base log
     (22, 1, 1): "k_blind_rotate_v4<1, true, 0, 4, false, 0>",
     (12, 3, 1): "k_blind_rotate_v4s<3, false, 0, 0>",
-    (10, 4, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (8, 5, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (7, 6, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (6, 7, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
-    (5, 8, 1): "k_blind_rotate_mw<fhei::V2, 2, 2, BrTv>",
+    (10, 4, 1): "k_blind_rotate_v4s<4, false, 0, 0>",
+    (8, 5, 1): "k_blind_rotate_v4s<5, false, 0, 0>",
+    (7, 6, 1): "k_blind_rotate_v4s<6, false, 0, 0>",
+    (6, 7, 1): "k_blind_rotate_v4s<7, false, 0, 0>",
+    (5, 8, 1): "k_blind_rotate_v4s<8, false, 0, 0>",
     (15, 2, 2): "k_blind_rotate_mb<2, 0, 15>",
     (23, 1, 2): "k_blind_rotate_mb<1, 0, 23>",
     # the multi-bit kernels with a run-time base log (other gadgets)
