@@ -252,41 +252,59 @@ def plan_cost(p: SchemeParams) -> float:
     return sum(BR_COST[(lv, grp)] for _, lv, grp in plan_gadgets(p))
 
 
+def _cheapest_plan(p: SchemeParams) -> SchemeParams:
+    """p (main gadget set) with the cheapest fast / fast2 choice of
+    FAST_GADGETS, then the cheapest mid / mid2 choice (by plan_cost)."""
+    beta, lvl = p.pbs_base_log, p.pbs_level
+    cands = [g for g in FAST_GADGETS if g != (beta, lvl, 1)]
+    choices = [(g,) for g in cands] + [(a, b) for a in cands for b in cands if a[:2] != b[:2]]
+    best = plan_cost(p)
+    for ch in choices:
+        kw = {"pbs_fast_base_log": ch[0][0], "pbs_fast_level": ch[0][1], "pbs_fast_group": ch[0][2]}
+        if len(ch) > 1:
+            kw.update(pbs_fast2_base_log=ch[1][0], pbs_fast2_level=ch[1][1], pbs_fast2_group=ch[1][2])
+        q = replace(p, **kw)
+        c = plan_cost(q)
+        if c < best - 1e-9:
+            p, best = q, c
+    if p.pbs_fast_level:
+        # then one or two mid gadgets: cheaper main gadgets of PBS_GADGETS,
+        # between the main and the fast one
+        mids = [(b, lv) for _, b, lv in PBS_GADGETS if lv < lvl]
+        q0 = p
+        for ch in [(m,) for m in mids] + [(a, b) for a in mids for b in mids if a[1] > b[1]]:
+            kw = {"pbs_mid_base_log": ch[0][0], "pbs_mid_level": ch[0][1]}
+            if len(ch) > 1:
+                kw.update(pbs_mid2_base_log=ch[1][0], pbs_mid2_level=ch[1][1])
+            q = replace(q0, **kw)
+            c = plan_cost(q)
+            if c < best - 1e-9:
+                p, best = q, c
+    return p
+
+
 def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
     """The gadget of PBS_GADGETS for width P; with fast, also up to two of
     FAST_GADGETS (other than the main gadget, in their order: fast, then
     fast2) for the sign rounds whose noise is barely amplified, the choice
     whose sign plan is cheapest by BR_COST, if it beats the single-gadget
     plan; then up to two mid gadgets (cheaper entries of PBS_GADGETS) for the
-    rounds between, if they make the plan cheaper still."""
-    for pmax, beta, lvl in PBS_GADGETS:
+    rounds between, if they make the plan cheaper still. A more precise main
+    gadget (the next entry of the table) is taken when its cheapest plan is
+    cheaper: a quieter first bootstrap can allow 4-bit digits (DESIGN.md
+    §3.6)."""
+    for i, (pmax, beta, lvl) in enumerate(PBS_GADGETS):
         if P <= pmax:
             p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
-            if fast and P >= 4:
-                cands = [g for g in FAST_GADGETS if g != (beta, lvl, 1)]
-                choices = [(g,) for g in cands] + [(a, b) for a in cands for b in cands if a[:2] != b[:2]]
-                best = plan_cost(p)
-                for ch in choices:
-                    kw = {"pbs_fast_base_log": ch[0][0], "pbs_fast_level": ch[0][1], "pbs_fast_group": ch[0][2]}
-                    if len(ch) > 1:
-                        kw.update(pbs_fast2_base_log=ch[1][0], pbs_fast2_level=ch[1][1], pbs_fast2_group=ch[1][2])
-                    q = replace(p, **kw)
-                    c = plan_cost(q)
-                    if c < best - 1e-9:
-                        p, best = q, c
-                if p.pbs_fast_level:
-                    # then one or two mid gadgets: cheaper main gadgets of
-                    # PBS_GADGETS, between the main and the fast one
-                    mids = [(b, lv) for _, b, lv in PBS_GADGETS if lv < lvl]
-                    q0 = p
-                    for ch in [(m,) for m in mids] + [(a, b) for a in mids for b in mids if a[1] > b[1]]:
-                        kw = {"pbs_mid_base_log": ch[0][0], "pbs_mid_level": ch[0][1]}
-                        if len(ch) > 1:
-                            kw.update(pbs_mid2_base_log=ch[1][0], pbs_mid2_level=ch[1][1])
-                        q = replace(q0, **kw)
-                        c = plan_cost(q)
-                        if c < best - 1e-9:
-                            p, best = q, c
+            if not (fast and P >= 4):
+                return p
+            p = _cheapest_plan(p)
+            best = plan_cost(p)
+            for _, b2, l2 in PBS_GADGETS[i + 1:i + 2]:
+                q = _cheapest_plan(SchemeParams(pbs_base_log=b2, pbs_level=l2, msg_bits=P))
+                c = plan_cost(q)
+                if c < best - 1e-9:
+                    p, best = q, c
             return p
     raise ValueError(f"accumulator width P={P} exceeds the supported 27 bits")
 

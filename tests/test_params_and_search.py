@@ -15,8 +15,11 @@ from fheicp.search import sharded_topk
 
 @pytest.mark.parametrize("pmax,beta,lvl", PBS_GADGETS)
 def test_gadget_table_has_margin(pmax, beta, lvl):
-    p = params_for_bits(pmax)
-    assert (p.pbs_base_log, p.pbs_level) == (beta, lvl)
+    from fheicp.params import SchemeParams, _cheapest_plan
+    # the table's gadget with its cheapest fast / mid gadgets (params_for_bits
+    # may still pick the next, more precise main gadget when that is cheaper)
+    p = _cheapest_plan(SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=pmax))
+    assert params_for_bits(pmax).pbs_level in (lvl, lvl + 1)
     # >= 9.2 sigma at the decision margin  <=>  p_fail <= 2^-64 per PBS, for
     # the digit sign extraction (1/16 margin) and the single-bit one (1/4)
     for method in ("digits", "bits"):
@@ -63,7 +66,7 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
         R = L.fhe_sign_schedule(cp, sched, 64)
         assert sign_schedule(p)[1] == oracle_lib.sign_schedule(d) == list(sched[:R]), d
     # the headline width: 4-bit digits at P = 16, 3-bit where 4 misses the bar
-    assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 3, 3, 3]
+    assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 4, 4, 3]
     assert sign_pbs_count(16) == 7
     assert noise_report(params_for_bits(16))["digit_bits"] == 4
 
@@ -77,8 +80,8 @@ def test_fast_gadget_plan():
     from fheicp.params import _plan_worst, plan_cost
     F, F2 = (15, 2, 2), (23, 1, 2)
     want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F, F2, (4, 0, 1)), 12: (F, F2, (4, 0, 1)),
-            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 1, 3)), 17: (F, F2, (3, 0, 5)), 18: (F, F2, (4, 1, 5)),
-            19: (F, F2, (4, 1, 5)), 21: (F, F2, (3, 3, 7))}
+            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 1, 3)), 17: (F, F2, (4, 1, 5)), 18: (F, F2, (4, 1, 5)),
+            19: (F, F2, (4, 1, 5))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
         assert p.pbs_mid_level == 0, P
@@ -107,8 +110,8 @@ def test_mid_gadget_plan():
     the plan is cheaper than the same gadgets without mids."""
     from dataclasses import replace
     from fheicp.params import _sched_worst, plan_cost, sign_schedule
-    want = {20: ((15, 2), None), 22: ((12, 3), None), 23: ((12, 3), None), 24: ((10, 4), (12, 3)), 25: ((10, 4), (12, 3)),
-            26: ((8, 5), (12, 3)), 27: ((8, 5), (12, 3))}
+    want = {20: ((15, 2), None), 21: ((12, 3), None), 22: ((12, 3), None), 23: ((12, 3), None),
+            24: ((8, 5), (12, 3)), 25: ((10, 4), (12, 3)), 26: ((8, 5), (12, 3)), 27: ((8, 5), (12, 3))}
     for P, (m1, m2) in want.items():
         p = params_for_bits(P)
         assert (p.pbs_mid_base_log, p.pbs_mid_level) == m1, P
@@ -127,8 +130,13 @@ def test_mid_gadget_plan():
         assert plan_cost(p) < plan_cost(nomid), P
     # C5's width: 1 main (6,7), 2 mid (8,5), 3 mid2 (12,3), 5 fast, 6 fast2
     assert sign_schedule(params_for_bits(26))[1] == [0, 3, 3, 4, 4, 4] + [1] * 5 + [2] * 6
-    # the headline and C3 widths have no mid gadget
-    assert params_for_bits(16).pbs_mid_level == 0 and params_for_bits(21).pbs_mid_level == 0
+    # the headline width has no mid gadget; C3's (P = 21) takes the more
+    # precise (10,4) main gadget, whose quieter first bootstrap allows 4-bit
+    # digits: 10 bootstraps instead of 13
+    assert params_for_bits(16).pbs_mid_level == 0
+    p21 = params_for_bits(21)
+    assert (p21.pbs_base_log, p21.pbs_level) == (10, 4)
+    assert sign_schedule(p21) == (4, [0, 3, 3, 1, 1, 1, 1, 2, 2, 2])
 
 
 def test_multibit_noise_model():
@@ -154,7 +162,8 @@ def test_sign_digit_bits_validation():
 
 def test_params_for_bits_limits():
     assert params_for_bits(11).pbs_level == 2
-    assert params_for_bits(21).pbs_level == 3
+    assert params_for_bits(21, fast=False).pbs_level == 3   # the table's gadget
+    assert params_for_bits(21).pbs_level == 4               # the cheaper plan's main gadget
     with pytest.raises(ValueError):
         params_for_bits(28)
 
