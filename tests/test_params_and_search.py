@@ -277,3 +277,33 @@ def test_processor_sharded_search_gloo(tmp_path, monkeypatch, world):
         for (k, t), g in zip(cases, got):
             want = [(ids[i], s) for i, s in Q.search(qp, qv, docs, k, t)]
             assert g == want, (k, t)
+
+
+@pytest.mark.parametrize("beta,lvl", [(12, 3), (10, 4), (8, 5), (7, 6), (6, 7), (5, 8)])
+def test_offset_digits_equal_sequential(beta, lvl):
+    """The deep v4s kernels re-extract each level's digit as
+    ((r' >> i beta) & (B - 1)) - B/2 from r' = r + sum_i (B/2) B^i, r the
+    rounded top L*beta bits; the other kernels and the oracle use the
+    sequential balanced decomposition (sign-extend beta bits, subtract,
+    next). Both are the digit representation of r mod B^L in [-B/2, B/2), so
+    they agree on every input: checked here on random words, near-ties and
+    the top of the range (numpy uint64, mod-2^64 like the kernels)."""
+    rng = np.random.default_rng(beta * 10 + lvl)
+    x = rng.integers(0, 2 ** 63, 200_000, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, 200_000, dtype=np.uint64)
+    prec = lvl * beta
+    x[:2000] = (np.arange(2000, dtype=np.uint64) << np.uint64(64 - prec - 1))   # rounding ties
+    x[2000:4000] = np.uint64(2 ** 64 - 1) - np.arange(2000, dtype=np.uint64)
+    r = ((x >> np.uint64(63 - prec)) + np.uint64(1)) >> np.uint64(1)
+    B = np.uint64(1 << beta)
+    seq = np.zeros((lvl, x.size), np.int64)
+    rr = r.copy()
+    for i in range(lvl):
+        low = ((rr >> np.uint64(i * beta)) & (B - np.uint64(1))).astype(np.int64)
+        d = np.where(low >= (1 << (beta - 1)), low - (1 << beta), low)
+        seq[lvl - 1 - i] = d
+        rr = rr - (d.astype(np.uint64) << np.uint64(i * beta))      # mod 2^64
+    coff = np.uint64(sum(1 << (i * beta + beta - 1) for i in range(lvl)))
+    rp = r + coff
+    for lv in range(lvl):
+        off = ((rp >> np.uint64((lvl - 1 - lv) * beta)) & (B - np.uint64(1))).astype(np.int64) - (1 << (beta - 1))
+        assert np.array_equal(off, seq[lv]), (beta, lvl, lv)
