@@ -68,8 +68,14 @@ struct fhe_ctx {
   int v4_dbg = 0;      // timing experiments only (FHEICP_V4_DBG), wrong results
   // i8-MFMA key switch: key byte planes and a digit/body workspace
   int8_t* ksk8 = nullptr;
-  void* ks_ws = nullptr;
+  void* ks_ws = nullptr;       // lane 0 (every caller stream)
   size_t ks_ws_bytes = 0;
+  void* ks_ws1 = nullptr;      // lane 1: the second half of a pipelined compare
+  size_t ks_ws1_bytes = 0;
+  // two streams and their events for the pipelined sign extraction of
+  // fhe_compare_batch (created on first use)
+  hipStream_t lane_st[2] = {nullptr, nullptr};
+  hipEvent_t lane_ev[3] = {nullptr, nullptr, nullptr};
   int ks_variant = 2;  // 2 = MFMA (default when ks_level == 4), 1 = VALU split-K
 };
 
@@ -451,9 +457,13 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
                       (void*)ctx->ksk_colsum, (void*)ctx->bsk_fft, (void*)ctx->tw, (void*)ctx->twist, ctx->ws,
                       (void*)ctx->bskf[0], (void*)ctx->bskf[1], (void*)ctx->bskf_fft[0], (void*)ctx->bskf_fft[1],
                       (void*)ctx->bskf[2], (void*)ctx->bskf[3], (void*)ctx->bskf_fft[2], (void*)ctx->bskf_fft[3],
-                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2,
+                      (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->ks_ws1, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2,
                       (void*)ctx->psi, (void*)ctx->mb_msg})
       (void)hipFree(ptr);
+    for (hipStream_t s : ctx->lane_st)
+      if (s) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : ctx->lane_ev)
+      if (e) (void)hipEventDestroy(e);
     free_ev(ctx->prof_br);
     for (auto& a : ctx->prof_brf) free_ev(a);
     free_ev(ctx->prof_ks);
@@ -832,33 +842,41 @@ static void prof_end(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t e1, in
   a.items += items;
 }
 
-int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
-                        uint64_t* d_small, void* stream) {
-  int rc = need_keys(ctx);
-  if (rc) return rc;
-  if (count < 0 || shift < 0 || shift > 63 || (count > 0 && (!d_big || !d_small)))
-    return fail(ctx, FHE_E_ARG, "bad keyswitch arguments");
-  if (count == 0) return FHE_OK;
+// the MFMA key switch's digit + body workspace of lane 0 or 1, grown to
+// `count` ciphertexts (a grow synchronises the device: callers that run two
+// lanes reserve both before launching on either)
+static int ks_reserve(fhe_ctx* ctx, int64_t count, int lane) {
   const fhe_params& p = ctx->p;
-  hipStream_t st = (hipStream_t)stream;
+  const int K = p.k * p.N * p.ks_level;
+  const size_t need = (size_t)((count + 15) / 16) * 16 * K + 8 * (size_t)count;
+  void*& ws = lane ? ctx->ks_ws1 : ctx->ks_ws;
+  size_t& have = lane ? ctx->ks_ws1_bytes : ctx->ks_ws_bytes;
+  if (need <= have) return FHE_OK;
+  if (ws) {
+    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, hipFree(ws));
+    ws = nullptr;
+  }
+  HIPCHK(ctx, hipMalloc(&ws, need));
+  have = need;
+  return FHE_OK;
+}
+
+static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
+                          uint64_t* d_small, hipStream_t st, int lane) {
+  const fhe_params& p = ctx->p;
   const int64_t tiles = (count + KS_TC - 1) / KS_TC;
   if (tiles > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
   if (ctx->ks_variant == 2) {
     const int K = p.k * p.N * p.ks_level, KB = K / 64, n1 = p.n + 1, NB = (n1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
     const int64_t ncb = (count + 15) / 16;
-    const size_t dbytes = (size_t)ncb * 16 * K, need = dbytes + 8 * (size_t)count;
-    if (need > ctx->ks_ws_bytes) {
-      if (ctx->ks_ws) {
-        HIPCHK(ctx, hipDeviceSynchronize());
-        HIPCHK(ctx, hipFree(ctx->ks_ws));
-        ctx->ks_ws = nullptr;
-      }
-      HIPCHK(ctx, hipMalloc(&ctx->ks_ws, need));
-      ctx->ks_ws_bytes = need;
-    }
+    const size_t dbytes = (size_t)ncb * 16 * K;
+    int rc = ks_reserve(ctx, count, lane);
+    if (rc) return rc;
     if (ncb > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
-    uint32_t* D = (uint32_t*)ctx->ks_ws;
-    u64* body = (u64*)((char*)ctx->ks_ws + dbytes);
+    void* ws = lane ? ctx->ks_ws1 : ctx->ks_ws;
+    uint32_t* D = (uint32_t*)ws;
+    u64* body = (u64*)((char*)ws + dbytes);
     hipEvent_t e1;
     prof_begin(ctx, ctx->prof_ks, st, &e1);
     ctx->prof_ks.kernel = "k_keyswitch_mfma";
@@ -880,6 +898,16 @@ int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int3
   prof_end(ctx, ctx->prof_ks, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
+}
+
+int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
+                        uint64_t* d_small, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (count < 0 || shift < 0 || shift > 63 || (count > 0 && (!d_big || !d_small)))
+    return fail(ctx, FHE_E_ARG, "bad keyswitch arguments");
+  if (count == 0) return FHE_OK;
+  return keyswitch_lane(ctx, d_big, count, shift, add_body, d_small, (hipStream_t)stream, 0);
 }
 
 #ifdef FHEICP_AB
@@ -1247,13 +1275,16 @@ int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_r
 }
 
 static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
-                        hipStream_t st) {
+                        hipStream_t st, int lane = 0) {
+  auto keyswitch = [&](int shift, uint64_t add) {
+    return keyswitch_lane(ctx, d_ct_v, count, shift, add, small, st, lane);
+  };
   const fhe_params& p = ctx->p;
   const int P = p.msg_bits, logN = log2i(p.N);
   int rc;
   if (P < 4) {
     for (int i = 0; i < P; ++i) {
-      if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - 1 - i, 1ull << 62, small, st))) return rc;
+      if ((rc = keyswitch(P - 1 - i, 1ull << 62))) return rc;
       if ((rc = launch_br(ctx, small, count, BrTv{1ull << (63 - P + i), 0, 0}, 1, nullptr, d_ct_v, nullptr,
                           (i == P - 1) ? d_sign : nullptr, st)))
         return rc;
@@ -1271,10 +1302,10 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
   auto digit = [&](int b, int c) -> int {
     int r;
     // digit MSB (bit b+c-1): sign bootstrap, ct_v -= [bit] * 2^(b+c-1) * Delta
-    if ((r = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - c, 1ull << (63 - c), small, st))) return r;
+    if ((r = keyswitch(P - b - c, 1ull << (63 - c)))) return r;
     if ((r = br(BrTv{1ull << (62 - P + b + c), 0, 0}, 1, nullptr))) return r;
     // bits [b, b+c-1): top bit is now 0 -> 2^(c-1)-slot staircase, output D' * 2^b * Delta
-    if ((r = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - c, 1ull << (63 - c), small, st))) return r;
+    if ((r = keyswitch(P - b - c, 1ull << (63 - c)))) return r;
     return br(BrTv{0, 1ull << (64 - P + b), logN - (c - 1)}, 2, nullptr);
   };
   int b = 0;
@@ -1285,12 +1316,51 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
     b = m;
   }
   for (; b < m; ++b) {
-    if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, P - b - 1, 1ull << 62, small, st))) return rc;
+    if ((rc = keyswitch(P - b - 1, 1ull << 62))) return rc;
     if ((rc = br(BrTv{1ull << (63 - P + b), 0, 0}, 1, nullptr))) return rc;
   }
   // sign = MSB of the top digit [P-d, P)
-  if ((rc = fhe_keyswitch_batch(ctx, d_ct_v, count, 0, 1ull << (63 - d), small, st))) return rc;
+  if ((rc = keyswitch(0, 1ull << (63 - d)))) return rc;
   return br(BrTv{1ull << 62, 0, 0}, 1, d_sign);
+}
+
+// The sign extraction of a large batch (>= PIPE_MIN ciphertexts) in two
+// halves on two streams: each half runs its key switches and bootstraps in
+// order, and the GPU overlaps one half's key switches and kernel tails with
+// the other half's bootstraps. Below PIPE_MIN (one or two waves of
+// workgroups) it stays on the caller's stream, so single-launch timings keep
+// their meaning. FHEICP_PIPE=0 turns it off (A/B runs).
+constexpr int64_t PIPE_MIN = 2048;
+static int sign_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
+                              hipStream_t st) {
+  static const bool off = [] {
+    const char* e = getenv("FHEICP_PIPE");
+    return e && atoi(e) == 0;
+  }();
+  if (count < PIPE_MIN || off) return sign_extract(ctx, d_ct_v, count, d_sign, small, st, 0);
+  const fhe_params& p = ctx->p;
+  const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
+  const int64_t c0 = ((count / 2) + 3) & ~(int64_t)3, c1 = count - c0;  // whole workgroups of 4
+  for (int l = 0; l < 2; ++l)
+    if (!ctx->lane_st[l]) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->lane_st[l], hipStreamNonBlocking));
+  for (int l = 0; l < 3; ++l)
+    if (!ctx->lane_ev[l]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->lane_ev[l], hipEventDisableTiming));
+  int rc = ks_reserve(ctx, c0, 0);
+  if (!rc) rc = ks_reserve(ctx, c1, 1);
+  if (rc) return rc;
+  HIPCHK(ctx, hipEventRecord(ctx->lane_ev[0], st));
+  for (int l = 0; l < 2; ++l) HIPCHK(ctx, hipStreamWaitEvent(ctx->lane_st[l], ctx->lane_ev[0], 0));
+  rc = sign_extract(ctx, d_ct_v, c0, d_sign, small, ctx->lane_st[0], 0);
+  if (!rc)
+    rc = sign_extract(ctx, d_ct_v + (size_t)c0 * Wb, c1, d_sign + (size_t)c0 * Wb, small + (size_t)c0 * Ws,
+                      ctx->lane_st[1], 1);
+  // the caller's stream waits for both halves (also on an error, so nothing
+  // queued on it can overtake work already launched on the lanes)
+  for (int l = 0; l < 2; ++l) {
+    HIPCHK(ctx, hipEventRecord(ctx->lane_ev[1 + l], ctx->lane_st[l]));
+    HIPCHK(ctx, hipStreamWaitEvent(st, ctx->lane_ev[1 + l], 0));
+  }
+  return rc;
 }
 
 int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, void* stream) {
@@ -1300,7 +1370,7 @@ int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_si
   if (count == 0) return FHE_OK;
   rc = ensure_ws(ctx, 8 * (size_t)count * fhe_small_lwe_words(&ctx->p));
   if (rc) return rc;
-  return sign_extract(ctx, d_ct_v, count, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream);
+  return sign_extract_batch(ctx, d_ct_v, count, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream);
 }
 
 int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_refreshed, uint64_t* d_sign,
@@ -1341,7 +1411,7 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   // computes the encrypted threshold bit [acc < T] exactly.
   rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
   if (rc) return rc;
-  rc = sign_extract(ctx, ctv, B, sgn, small, st);
+  rc = sign_extract_batch(ctx, ctv, B, sgn, small, st);
   if (rc) return rc;
   rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
   if (rc) return rc;
@@ -1372,7 +1442,7 @@ int fhe_compare_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_
   if (rc) return rc;
   rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
   if (rc) return rc;
-  rc = sign_extract(ctx, ctv, B, sgn, small, st);
+  rc = sign_extract_batch(ctx, ctv, B, sgn, small, st);
   if (rc) return rc;
   rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
   if (rc) return rc;
@@ -1399,7 +1469,7 @@ int fhe_threshold_batch(fhe_ctx* ctx, const uint64_t* d_ct_acc, int64_t count, i
   hipLaunchKernelGGL(k_lwe_affine, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, d_ct_acc, count, (int)Wb,
                      (u64)1, (u64)0 - ((u64)T << (64 - p.msg_bits)), ctv);
   HIPCHK(ctx, hipGetLastError());
-  rc = sign_extract(ctx, ctv, count, d_bit, small, st);
+  rc = sign_extract_batch(ctx, ctv, count, d_bit, small, st);
   if (rc) return rc;
   // [acc >= T] = 1 - [v < 0]: negate the sign ciphertext and add 2^63 to its body
   hipLaunchKernelGGL(k_lwe_affine, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, d_bit, count, (int)Wb,
