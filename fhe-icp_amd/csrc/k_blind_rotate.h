@@ -334,13 +334,19 @@ __device__ __forceinline__ void decompose_v4(typename v4::Acc<A32>::T x, int bet
       if (i + 1 < L) r -= (uint32_t)di << (i * beta);
     }
   } else {
-    u64 r = ((x >> (63 - prec)) + 1) >> 1;
+    // the same digits (round half up, then balanced), read without the
+    // carry chain: adding 2^(63-prec) (the rounding) and the balancing offset
+    // sum_i (B/2) B^i at bit 64-prec makes each digit its plain beta-bit field
+    // minus B/2 (the representation mod B^L is unique; a carry out of bit 63
+    // is a multiple of B^L). One 64-bit add, then a shift, mask and subtract
+    // per digit, against a shift pair, a 64-bit subtract and more per digit.
+    u64 k = (u64)1 << (63 - prec);
 #pragma unroll
-    for (int i = 0; i < L; ++i) {
-      const int64_t di = (int64_t)(r << (64 - (i + 1) * beta)) >> (64 - beta);
-      d[L - 1 - i] = (int)di;
-      if (i + 1 < L) r -= (u64)di << (i * beta);
-    }
+    for (int i = 0; i < L; ++i) k += (u64)1 << (64 - prec + i * beta + beta - 1);
+    const u64 sx = x + k;
+#pragma unroll
+    for (int i = 0; i < L; ++i)
+      d[L - 1 - i] = (int)((uint32_t)(sx >> (64 - prec + i * beta)) & ((1u << beta) - 1u)) - (1 << (beta - 1));
   }
 }
 
@@ -919,17 +925,23 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
   // From L = 3 the level loop stays rolled: unrolled, the compiler hoists
   // work across levels and spills (28 bytes at L = 3, 172-532 at L = 4-7;
   // rolled: 0 at L = 3). From L = 4 the digits are not kept per level but
-  // re-extracted from the rounded difference plus the balancing offset
-  // sum_i (B/2) B^i: digit_i = ((r' >> i beta) & (B - 1)) - B/2 equals the
-  // sequential balanced decomposition (the same representation mod B^L).
+  // re-extracted from the difference plus the rounding and balancing
+  // constant (decompose_v4's offset form): each is a plain beta-bit field
+  // minus B/2, the same digits as the sequential balanced decomposition.
   constexpr bool ROLL = L >= 3;
   constexpr bool RECOMP = L >= 4;
   static_assert(!RECOMP || !A32, "re-extracted digits are for the 64-bit accumulators");
+  // (decompose_v4's offset form: the rounding and balancing constant added
+  // once, each level's digit a plain field of the sum)
+  const int prec = L * bta;
   u64 coff = 0;
-  if constexpr (RECOMP)
-    for (int l = 0; l < L; ++l) coff += (u64)1 << (l * bta + bta - 1);
+  if constexpr (RECOMP) {
+    coff = (u64)1 << (63 - prec);
+    for (int l = 0; l < L; ++l) coff += (u64)1 << (64 - prec + l * bta + bta - 1);
+  }
   auto digit_at = [&](u64 rr, int lv) -> double {
-    return (double)((int)((rr >> ((L - 1 - lv) * bta)) & ((1u << bta) - 1u)) - (1 << (bta - 1)));
+    return (double)((int)((uint32_t)(rr >> (64 - prec + (L - 1 - lv) * bta)) & ((1u << bta) - 1u)) -
+                    (1 << (bta - 1)));
   };
   c64 kb[2][WPC];  // this level's rows: [slot t][row]
   for (int i = 0; i < n; ++i) {
@@ -954,7 +966,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
         for (int h = 0; h < 2; ++h) {
           const uint32_t src = (uint32_t)((s + h * S) * 64 + lane - (int)a) & (2 * N - 1);
           const u64 x = (u64)((src >= (uint32_t)N ? (T)0 - rot[s + h * S] : rot[s + h * S]) - acc[s + h * S]);
-          rr[s + h * S] = (((x >> (63 - L * bta)) + 1) >> 1) + coff;
+          rr[s + h * S] = x + coff;
         }
         v[s] = {digit_at(rr[s], 0), digit_at(rr[s + S], 0)};
       } else {
