@@ -318,7 +318,7 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);
 /* The kernel last launched for that bucket, as rocprofv3 names it (e.g.
- * "k_blind_rotate_v4<2, true, 0, 4, false>", "k_blind_rotate_mw<fhei::V2, 2, 2>",
+ * "k_blind_rotate_v4<2, true, 0, 4, false, 15>", "k_blind_rotate_mb<1, 0, 23>",
  * "k_keyswitch_mfma"); "" before any launch. Not reset by fhe_profile_read. */
 int fhe_profile_kernel_name(fhe_ctx* ctx, const char* kernel, char* h_buf, size_t len);
 /* "libfheicp gfx950 ab=0" for the shipped build; ab=1 for A/B builds
