@@ -1,8 +1,8 @@
 #!/bin/bash
 # v2 against the key-stationary v4s kernels at the deep gadgets (L = 3..8):
 # blind-rotation time per 1024 and output noise against the model
-# (tools/prof_br.py --gadget), product library vs libfheicp_deep.so
-# (tools/build_variant.sh deep -DFHEICP_V4S_DEEP).
+# (tools/prof_br.py --gadget): the libraries in $LIBS (default: an A/B
+# build libfheicp_prev.so against the product library).
 set -u -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"
 for g in ${GADGETS:-12,3 10,4 8,5 7,6 6,7 5,8}; do

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time and noise of the fast-gadget bootstraps (fhe_pbs_gadget_batch) at the
-P=21 parameter set (fast (15,2), fast2 (23,1)): classic vs multi-bit
-(FHEICP_MB), and A/B library builds (--lib). Prints per-launch HIP-event ms
+P=21 parameter set (fast (15,2), fast2 (23,1), both multi-bit),
+and A/B library builds (--lib). Prints per-launch HIP-event ms
 and the output noise against the model."""
 import argparse
 import math
