@@ -1,5 +1,5 @@
 #!/bin/bash
-# classic v4 vs key-stationary v4s (FHEICP_V4S=1) for the main gadgets, and
+# classic v4 vs key-stationary v4s (FHEICP_V4S=1) for the classic gadgets
 # (needs the A/B build: tools/build_variant.sh ab -DFHEICP_AB)
 set -o pipefail
 for rep in 1 2; do
