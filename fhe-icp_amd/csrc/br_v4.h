@@ -364,7 +364,24 @@ struct Acc<false> {
   using T = u64;
   static __device__ __forceinline__ T from64(u64 x) { return x; }
   static __device__ __forceinline__ u64 to64(T x) { return x; }
-  static __device__ __forceinline__ T from_f64(double z) { return f64_to_torus(z); }
+  // round(z * 2^64) mod 2^64 from t = z (the FFT-domain BSK carries the
+  // 2^-64 here too), bit-identical to f64_to_torus(z * 2^64) for any z:
+  // f = z - rint(z) is exact, F = f * 2^32 splits into h = rint(F) (the low
+  // mantissa word of F + 1.5 * 2^52) and r = F - h (exact, |r| <= 1/2),
+  // and bits(r * 2^32 + 1.5 * 2^52) = bits(1.5 * 2^52) + rint(r * 2^32).
+  // 8 f64 + 4 integer ops against f64_to_torus's 9 + 6 (split via floor,
+  // a sign fix-up and two conversions).
+  static __device__ __forceinline__ T from_f64(double z) {
+#ifdef FHEICP_TORUS_SPLIT  // A/B build only (tools/build_variant.sh)
+    return f64_to_torus(__builtin_ldexp(z, 64));
+#endif
+    constexpr double M = 6755399441055744.0;
+    const double F = __builtin_ldexp(z - __builtin_rint(z), 32);
+    const double t1 = F + M;
+    const double t2 = __builtin_ldexp(F - (t1 - M), 32) + M;
+    const u64 hi = (u64)(uint32_t)__builtin_bit_cast(u64, t1) << 32;
+    return hi + (__builtin_bit_cast(u64, t2) - 0x4338000000000000ull);
+  }
 };
 
 }  // namespace v4

@@ -287,8 +287,8 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
 // ---- blind rotation v4 (br_v4.h): a wave per GLWE component ---------------
 // BSK conversion: one wave per polynomial, stored [poly][u][lane] (layout LC
 // of the forward transform) and scaled by 1/M.
-// scale = 1/M, times 2^-64 for the 32-bit-accumulator kernels (Acc<true>
-// reads the torus from fract(z), so the products arrive already scaled)
+// scale = 2^-64 / M: both accumulator widths (br_v4.h Acc) read the torus
+// from z - floor(z) or z - rint(z), so the products arrive already scaled
 __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bsk, int npoly,
                                                       const c64* __restrict__ tw4, c64* __restrict__ out,
                                                       double scale) {

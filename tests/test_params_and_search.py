@@ -307,3 +307,31 @@ def test_offset_digits_equal_sequential(beta, lvl):
     for lv in range(lvl):
         off = ((rp >> np.uint64((lvl - 1 - lv) * beta)) & (B - np.uint64(1))).astype(np.int64) - (1 << (beta - 1))
         assert np.array_equal(off, seq[lv]), (beta, lvl, lv)
+
+
+def test_two_word_torus_rounding_equals_split():
+    """The 64-bit-accumulator kernels (br_v4.h Acc<false>::from_f64) read
+    round(z 2^64) mod 2^64 as h 2^32 + rint(r 2^32), h = rint(F) and r = F - h
+    for F = (z - rint(z)) 2^32, with both roundings done by adding 1.5 2^52
+    and reading mantissa bits; wave_fft.h f64_to_torus (the form it replaces)
+    splits round(v) mod 2^64 through floor. Restated in numpy on random
+    magnitudes, exact ties and tiny values: the two agree bit for bit."""
+    rng = np.random.default_rng(7)
+    z = rng.standard_normal(300_000) * np.exp2(rng.integers(-70, 40, 300_000))
+    z[:1000] = (np.arange(1000) - 500 + 0.5) * 2.0 ** -64             # ties at 2^-64
+    z[1000:2000] = (np.arange(1000) - 500 + 0.5) * 2.0 ** -20
+    z[2000:2010] = [0.0, -0.0, 0.5, -0.5, 1.5, -2.5, 2.0 ** 30, -(2.0 ** 30), 2.0 ** 60, 2.0 ** -1074]
+    M = 6755399441055744.0
+    bits = lambda a: a.view(np.uint64)
+    F = np.ldexp(z - np.rint(z), 32)
+    t1 = F + M
+    t2 = np.ldexp(F - (t1 - M), 32) + M
+    new = ((bits(t1) & np.uint64(0xFFFFFFFF)) << np.uint64(32)) + (bits(t2) - np.uint64(0x4338000000000000))
+    v = np.ldexp(z, 64)                                               # f64_to_torus(v)
+    m = np.rint(v * 2.0 ** -64)
+    r = np.rint(v - m * 2.0 ** 64)        # exact for these |v| (numpy has no fma; m 2^64 is exact)
+    hi = np.floor(r * 2.0 ** -32)
+    lo = r - hi * 2.0 ** 32
+    hu = np.where(hi >= 2.0 ** 31, hi - 2.0 ** 32, hi).astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    old = (hu << np.uint64(32)) + lo.astype(np.uint64)
+    assert np.array_equal(new, old)
