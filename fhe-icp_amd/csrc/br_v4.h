@@ -211,8 +211,9 @@ __device__ __forceinline__ void idft8(c64 (&v)[S]) {
 // lane twiddles of pass PS (0 = A: elements 0..7, entries m; 1 = B: elements
 // 1..7, entries 7 + m), in two batches of LDS reads to bound register use;
 // DBG bit 0 takes them from wf
-template <int PS, bool INV, int DBG = 0>
-__device__ __forceinline__ void lane_tw(c64 (&v)[S], const c64* twl, int lane, c64 wf) {
+// (NR > 0: pass A's first NR entries come from treg, kept in registers)
+template <int PS, bool INV, int DBG = 0, int NR = 0>
+__device__ __forceinline__ void lane_tw(c64 (&v)[S], const c64* twl, int lane, c64 wf, const c64* treg = nullptr) {
   constexpr int M0 = PS == 0 ? 0 : 1;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -220,7 +221,10 @@ __device__ __forceinline__ void lane_tw(c64 (&v)[S], const c64* twl, int lane, c
     c64 T[4];
 #pragma unroll
     for (int m = m0; m <= m1; ++m)
-      T[m - m0] = (DBG & 1) ? wf : PS == 0 ? twl[m * 64 + lane] : twl[NTA + (m - 1) * 8 + lb_low3(lane)];
+      T[m - m0] = (DBG & 1)            ? wf
+                  : (PS == 0 && m < NR) ? treg[m]
+                  : PS == 0             ? twl[m * 64 + lane]
+                                        : twl[NTA + (m - 1) * 8 + lb_low3(lane)];
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int m = bitrev3(u);
@@ -304,11 +308,12 @@ __device__ __forceinline__ void swap_lb(c64 (&v)[S]) {
 
 // folded coefficient pairs (a_t + i a_{t+M}), natural order (LA) -> LC;
 // includes the negacyclic twist w^t
-template <int DBG = 0>
-__device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {}) {
+template <int DBG = 0, int NR = 0>
+__device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {},
+                                        const c64* treg = nullptr) {
   fold8<false>(v);
   dft8(v);
-  lane_tw<0, false, DBG>(v, twl, lane, wf);
+  lane_tw<0, false, DBG, NR>(v, twl, lane, wf, treg);
   if constexpr ((DBG & 8) == 0) swap_lb(v);
   dft8(v);
   lane_tw<1, false, DBG>(v, twl, lane, wf);
@@ -316,14 +321,15 @@ __device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, i
   dft8(v);
 }
 // LC -> natural order (LA), times M, untwisted
-template <int DBG = 0>
-__device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {}) {
+template <int DBG = 0, int NR = 0>
+__device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {},
+                                        const c64* treg = nullptr) {
   idft8(v);
   relayout<R2I, LC, LB, DBG>(v, scr, lane);
   lane_tw<1, true, DBG>(v, twl, lane, wf);
   idft8(v);
   if constexpr ((DBG & 8) == 0) swap_lb(v);
-  lane_tw<0, true, DBG>(v, twl, lane, wf);
+  lane_tw<0, true, DBG, NR>(v, twl, lane, wf, treg);
   idft8(v);
   fold8<true>(v);
 }

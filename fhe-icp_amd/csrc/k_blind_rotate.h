@@ -698,6 +698,16 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
 
   fill_tables(twl, tw4, tid, NT);
   for (int x = tid; x < NPSI; x += NT) psil[x] = psi[x];
+#ifndef FHEICP_MB_TREG  // A/B builds only (tools/build_variant.sh)
+#define FHEICP_MB_TREG 4
+#endif
+  // pass-A lane twiddles m < NR held in registers for the whole rotation
+  // (L = 1 only: 154 -> 162 VGPRs, 8 fewer LDS reads per step; mb<1,0,23>
+  // 4.02 -> 3.97 ms per 1024, round 2; NR = 2 was slower, 6 and 8 no better)
+  constexpr int NR = L == 1 ? FHEICP_MB_TREG : 0;
+  c64 treg[NR > 0 ? NR : 1];
+#pragma unroll
+  for (int m = 0; m < NR; ++m) treg[m] = tw4[m * 64 + lane];
   for (int x = tid; x < G * np; x += NT) {
     const int gg = x / np, jj = x - gg * np;
     const int64_t cc = (int64_t)blockIdx.x * G + gg;
@@ -772,7 +782,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       };
       // (loading the first slot's rows before the transform instead, at L = 1:
       // 4.06 vs 4.04 ms per 1024, not kept)
-      forward(v, twl, slot, lane);
+      forward<0, NR>(v, twl, slot, lane, {}, treg);
       V4_STAMP(2 + 4 * lv);
 #pragma unroll
       for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
@@ -824,7 +834,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
     c64 ov[S];
 #pragma unroll
     for (int u = 0; u < S; ++u) ov[u] = slot[u * 64 + lane];
-    inverse(ov, twl, slot, lane);
+    inverse<0, NR>(ov, twl, slot, lane, {}, treg);
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       acc[u] += AT::from_f64(ov[u].x);
