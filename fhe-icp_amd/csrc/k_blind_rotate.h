@@ -369,6 +369,29 @@ __device__ unsigned long long g_v4_span[2048][3];
 // relayout, 16 no LDS rotation, 32 no LDS reads of the other components,
 // 128 phase timestamps (results correct).
 constexpr int FL_SYNC = 1;
+// Wave priorities across the barriers of a step (k_blind_rotate_v4 / _mb /
+// _v4s): raised right after each barrier and lowered half-way through the two
+// long phases (after the inverse transform; after the first of two product
+// halves), so the waves of a SIMD that are behind issue first and the three
+// reach the next barrier together instead of the last one running alone.
+// FHEICP_{V4,MB,V4S}_PRIO = 0 turns it off (A/B builds).
+#ifndef FHEICP_MB_PRIO
+#define FHEICP_MB_PRIO 1
+#endif
+#ifndef FHEICP_V4S_PRIO
+#define FHEICP_V4S_PRIO 1
+#endif
+#ifndef FHEICP_V4_PRIO
+#define FHEICP_V4_PRIO 1
+#endif
+#define BR_PRIO(EN, p)                                 \
+  do {                                                 \
+    if constexpr ((EN) != 0) __builtin_amdgcn_s_setprio(p); \
+  } while (0)
+#define MB_PRIO(p) BR_PRIO(FHEICP_MB_PRIO, p)
+#define V4S_PRIO(p) BR_PRIO(FHEICP_V4S_PRIO, p)
+#define V4_PRIO(p) BR_PRIO(FHEICP_V4_PRIO, p)
+
 template <int L, bool A32, int DBG = 0, int G = 2, bool FL = false, int BETA = 0>
 __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
                                                               int beta, const c64* __restrict__ bsk,
@@ -543,9 +566,11 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
           lds_barrier();
         }
       }
+      V4_PRIO(3);
       V4_STAMP(4 + 5 * lv);
 #pragma unroll
       for (int ci = 0; ci < K; ++ci) {
+        if (ci == 1) V4_PRIO(0);
         const int cin = comp + 1 + ci >= WPC ? comp + 1 + ci - WPC : comp + 1 + ci;
         const c64* fs = ctslots + cin * SCR;
         const int gp = Gi + ((cin * L + lv) * WPC + comp) * M;
@@ -571,6 +596,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
           lds_barrier();
         }
       }
+      V4_PRIO(3);
       V4_STAMP(6 + 5 * lv);
     }
     if constexpr (FL && (DBG & 4) == 0) ct_wait(fR, 3 * phase);
@@ -581,6 +607,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       acc[u] += AT::from_f64(mac[u].x);
       acc[u + S] += AT::from_f64(mac[u].y);
     }
+    V4_PRIO(0);
     V4_STAMP(13);
     if constexpr ((DBG & 128) != 0) stamp_[15] = __builtin_amdgcn_s_memrealtime();
     if constexpr ((DBG & 128) != 0)
@@ -789,6 +816,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       load(0, kb[0]);
       V4_STAMP(3 + 4 * lv);
       lds_barrier();
+      MB_PRIO(3);
       V4_STAMP(4 + 4 * lv);
       // slot 2g+1's exponent is slot 2g's plus 1024 (bitrev3(2g+1) =
       // bitrev3(2g) + 4): its table position is slot 2g's with bit 10
@@ -799,7 +827,10 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       for (int t = 0; t < 2; ++t) {
         // the second slot's rows load when it starts: prefetching them with
         // the first slot's spilled at L = 2 (10.25 vs 7.36 ms per 1024)
-        if (t == 1) load(1, kb[1]);
+        if (t == 1) {
+          MB_PRIO(0);
+          load(1, kb[1]);
+        }
         const int u = 2 * g + t;
 #pragma unroll
         for (int gg = 0; gg < G; ++gg) {
@@ -823,6 +854,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       }
       V4_STAMP(5 + 4 * lv);
       lds_barrier();
+      MB_PRIO(3);
     }
     // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
 #pragma unroll
@@ -830,6 +862,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
 #pragma unroll
       for (int t = 0; t < 2; ++t) xbuf[(gg * WPC + comp) * SCR + (2 * g + t) * 64 + lane] = o[gg][t];
     lds_barrier();
+    MB_PRIO(3);
     V4_STAMP(10);
     c64 ov[S];
 #pragma unroll
@@ -840,6 +873,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       acc[u] += AT::from_f64(ov[u].x);
       acc[u + S] += AT::from_f64(ov[u].y);
     }
+    MB_PRIO(0);
     V4_STAMP(11);
     if constexpr ((DBG & 128) != 0)
       if (blockIdx.x == 0 && w == (DBG >> 8) && j >= 100 && j < 104 && lane < 16) {
@@ -1017,9 +1051,11 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       load(i, lv, kb);
       V4_STAMP(3 + 4 * lv);
       lds_barrier();
+      V4S_PRIO(3);
       V4_STAMP(4 + 4 * lv);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
+        if (t == 1) V4S_PRIO(0);
         const int u = 2 * g + t;
 #pragma unroll
         for (int gg = 0; gg < G; ++gg) {
@@ -1035,6 +1071,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       }
       V4_STAMP(5 + 4 * lv);
       lds_barrier();
+      V4S_PRIO(3);
     }
     // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
 #pragma unroll
@@ -1042,6 +1079,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
 #pragma unroll
       for (int t = 0; t < 2; ++t) xbuf[(gg * WPC + comp) * SCR + (2 * g + t) * 64 + lane] = o[gg][t];
     lds_barrier();
+    V4S_PRIO(3);
     V4_STAMP(10);
     c64 ov[S];
 #pragma unroll
@@ -1052,6 +1090,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       acc[u] += AT::from_f64(ov[u].x);
       acc[u + S] += AT::from_f64(ov[u].y);
     }
+    V4S_PRIO(0);
     V4_STAMP(11);
     if constexpr ((DBG & 128) != 0)
       if (blockIdx.x == 0 && w == (DBG >> 8) && i >= 100 && i < 104 && lane < 16) {
