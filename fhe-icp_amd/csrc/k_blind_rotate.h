@@ -391,6 +391,18 @@ constexpr int FL_SYNC = 1;
 #define MB_PRIO(p) BR_PRIO(FHEICP_MB_PRIO, p)
 #define V4S_PRIO(p) BR_PRIO(FHEICP_V4S_PRIO, p)
 #define V4_PRIO(p) BR_PRIO(FHEICP_V4_PRIO, p)
+// Finer steps down the long phase (2 after the inverse, 1 after the digits)
+// pay at L = 2, 3 (v4 (15,2) 9.26 -> 9.13, mb (15,2) 6.56 -> 6.48, v4s (12,3)
+// 13.96 -> 13.72 ms) and cost at L = 1 and L >= 4 (mb (23,1) 3.81 -> 3.83,
+// v4s (8,5) 20.27 -> 20.53, (6,7) 26.8 -> 27.2); FHEICP_PRIO_FINE = 0 / 1
+// forces either (A/B builds)
+#ifndef FHEICP_PRIO_FINE
+#define FHEICP_PRIO_FINE -1
+#endif
+template <int L>
+__device__ constexpr bool br_prio_fine() {
+  return FHEICP_PRIO_FINE < 0 ? (L == 2 || L == 3) : FHEICP_PRIO_FINE != 0;
+}
 
 template <int L, bool A32, int DBG = 0, int G = 2, bool FL = false, int BETA = 0>
 __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v4(const u64* __restrict__ small, int64_t count, int n,
@@ -491,6 +503,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
     }
 
     V4_STAMP(1);
+    if constexpr (br_prio_fine<L>()) V4_PRIO(1);
     c64 mac[S];
 #pragma unroll
     for (int u = 0; u < S; ++u) mac[u] = {0.0, 0.0};
@@ -607,7 +620,7 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
       acc[u] += AT::from_f64(mac[u].x);
       acc[u + S] += AT::from_f64(mac[u].y);
     }
-    V4_PRIO(0);
+    V4_PRIO(br_prio_fine<L>() ? 2 : 0);
     V4_STAMP(13);
     if constexpr ((DBG & 128) != 0) stamp_[15] = __builtin_amdgcn_s_memrealtime();
     if constexpr ((DBG & 128) != 0)
@@ -785,6 +798,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
     }
     V4_STAMP(1);
+    if constexpr (br_prio_fine<L>()) MB_PRIO(1);
     c64 o[G][2];  // products of the quarter, per ciphertext
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
@@ -873,7 +887,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       acc[u] += AT::from_f64(ov[u].x);
       acc[u + S] += AT::from_f64(ov[u].y);
     }
-    MB_PRIO(0);
+    MB_PRIO(br_prio_fine<L>() ? 2 : 0);
     V4_STAMP(11);
     if constexpr ((DBG & 128) != 0)
       if (blockIdx.x == 0 && w == (DBG >> 8) && j >= 100 && j < 104 && lane < 16) {
@@ -1027,6 +1041,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       }
     }
     V4_STAMP(1);
+    if constexpr (br_prio_fine<L>()) V4S_PRIO(1);
     c64 o[G][2];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
@@ -1090,7 +1105,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       acc[u] += AT::from_f64(ov[u].x);
       acc[u + S] += AT::from_f64(ov[u].y);
     }
-    V4S_PRIO(0);
+    V4S_PRIO(br_prio_fine<L>() ? 2 : 0);
     V4_STAMP(11);
     if constexpr ((DBG & 128) != 0)
       if (blockIdx.x == 0 && w == (DBG >> 8) && i >= 100 && i < 104 && lane < 16) {
