@@ -739,11 +739,13 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
   fill_tables(twl, tw4, tid, NT);
   for (int x = tid; x < NPSI; x += NT) psil[x] = psi[x];
 #ifndef FHEICP_MB_TREG  // A/B builds only (tools/build_variant.sh)
-#define FHEICP_MB_TREG 4
+#define FHEICP_MB_TREG 8
 #endif
   // pass-A lane twiddles m < NR held in registers for the whole rotation
-  // (L = 1 only: 154 -> 162 VGPRs, 8 fewer LDS reads per step; mb<1,0,23>
-  // 4.02 -> 3.97 ms per 1024, round 2; NR = 2 was slower, 6 and 8 no better)
+  // (L = 1 only). NR = 4: 154 -> 162 VGPRs, 8 fewer LDS reads per step, mb<1,0,23>
+  // 4.02 -> 3.97 ms per 1024 (NR = 2 slower, 6 and 8 no better then). With the
+  // wave priorities of BR_PRIO the kernel fell to 148 VGPRs, and all eight fit:
+  // 3.77 -> 3.73 ms (NR = 6: 3.75; profiles/r02g_treg_ab.txt)
   constexpr int NR = L == 1 ? FHEICP_MB_TREG : 0;
   c64 treg[NR > 0 ? NR : 1];
 #pragma unroll
