@@ -1062,6 +1062,9 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
       // (this level's rows loaded before the transform, or the next level's
       // during the products, measured slower: FHEICP_V4S=1 A/B, round 2)
       forward(v, twl, slot, lane);
+      // (12,3): a drop after the deeper levels' transforms too (13.67 -> 13.30 ms per
+      // 1000 at C5); it costs 1-2% at L = 2 and L >= 4 (profiles/r02h_prio_fwd_ab.txt)
+      if (L == 3 && lv > 0) V4S_PRIO(1);
       V4_STAMP(2 + 4 * lv);
 #pragma unroll
       for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
