@@ -82,6 +82,11 @@ class BatchConfig:
     embedding_bits: Optional[int] = None     # n_e (default: n_bits)
     embedding_scale: Optional[float] = None  # s_e (default: calibrated on training embeddings)
     corpus_path: Optional[str] = None        # fheicp.persist corpus file: load, or save after creation
+    # the secret keys of model_path / corpus_path files are Fernet-wrapped
+    # under this password (default: $FHE_MASTER_PASSWORD, fheicp.persist);
+    # without one, saving a corpus needs allow_plaintext_secrets=True
+    password: Optional[str] = None
+    allow_plaintext_secrets: bool = False
 
     def __post_init__(self):
         if self.batch_size < 1:
@@ -151,16 +156,19 @@ class BatchProcessor:
         if km_model is not None:
             m = km_model
         elif cfg.model_path and os.path.exists(cfg.model_path):
-            m = FHESimilarityModel.load_compiled(cfg.model_path, device=cfg.device) if needs_keys else None
+            m = FHESimilarityModel.load_compiled(cfg.model_path, device=cfg.device,
+                                                 password=cfg.password) if needs_keys else None
             if m is None:
                 from fheicp import persist
                 from fheicp.sklearn import LinearRegression
-                qp, _, _ = persist.load_model(cfg.model_path)
+                # the clear modes read only the quantisation: no password needed
+                qp, _, _ = persist.load_model(cfg.model_path, keys=False)
                 m = FHESimilarityModel(input_dim=len(qp.coef), n_bits=qp.n_bits, device=cfg.device)
                 m.model = LinearRegression.from_quant_params(qp, device=cfg.device)
             if needs_keys and not m.compiled:
                 m.compile(None, key_seed=cfg.key_seed)
         else:
+            self._check_corpus_secret()
             m = FHESimilarityModel(input_dim=cfg.input_dim, n_bits=cfg.n_bits, device=cfg.device, seed=cfg.seed)
             X, _ = m.train()
             if needs_keys:
@@ -189,14 +197,26 @@ class BatchProcessor:
             logger.info("key manager: %s; training a new model", e)
             return None
 
+    def _check_corpus_secret(self):
+        """A corpus that will be saved needs a password for its secret keys
+        (or the explicit plaintext opt-in): fail before the keygen, not after."""
+        cfg = self.config
+        if not (cfg.store_ciphertexts and cfg.fhe == "execute" and cfg.corpus_path) or os.path.exists(cfg.corpus_path):
+            return
+        from fheicp.persist import _password
+        if _password(cfg.password) is None and not cfg.allow_plaintext_secrets:
+            raise ValueError("saving the encrypted corpus needs a password (BatchConfig.password or "
+                             "$FHE_MASTER_PASSWORD) or BatchConfig.allow_plaintext_secrets=True")
+
     def _init_corpus(self, m):
         """Load (config.corpus_path) or create the encrypted-corpus engine."""
         from fheicp import persist
         from fheicp.corpus import CorpusQuant, EncryptedCorpus
         cfg = self.config
         if cfg.corpus_path and os.path.exists(cfg.corpus_path):
-            self.corpus_engine = persist.load_corpus(cfg.corpus_path, device=cfg.device)
+            self.corpus_engine = persist.load_corpus(cfg.corpus_path, device=cfg.device, password=cfg.password)
             return
+        self._check_corpus_secret()
         qp = m.model.quant_params
         if cfg.embedding_scale is not None:
             cq = CorpusQuant(qp, int(cfg.embedding_bits or qp.n_bits), float(cfg.embedding_scale))
@@ -206,7 +226,8 @@ class BatchProcessor:
             cq = CorpusQuant.calibrate(qp, np.concatenate([e1, e2]), cfg.embedding_bits)
         self.corpus_engine = EncryptedCorpus(cq).compile(key_seed=cfg.key_seed, device=cfg.device)
         if cfg.corpus_path:
-            persist.save_corpus(cfg.corpus_path, self.corpus_engine)
+            persist.save_corpus(cfg.corpus_path, self.corpus_engine, password=cfg.password,
+                                allow_plaintext_secrets=cfg.allow_plaintext_secrets)
 
     def _require_model(self) -> FHESimilarityModel:
         if self.fhe_model is None:

@@ -497,14 +497,17 @@ static int need_keys(fhe_ctx* ctx) {
 // blind-rotation kernel for a gadget: the requested variant (4 unless
 // FHEICP_BR_VARIANT), falling back to v2 where v4 does not apply
 // the v4 kernel keeps 32-bit accumulators for this gadget
+// (the shipped 32-bit kernels exist for levels 1 and 2 only: a level-3
+// gadget with L*beta <= 31, e.g. (10,3), runs on the 64-bit v4s<3> kernel,
+// whose noise the model's 2^32 rounding term then over-counts)
 static bool v4_a32(const fhe_ctx* ctx, const fhe_params& q) {
-  return q.pbs_level * q.pbs_base_log <= 31 && !ctx->v4_a64;
+  return q.pbs_level <= 2 && q.pbs_level * q.pbs_base_log <= 31 && !ctx->v4_a64;
 }
 
 static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
   // v4 layout: the v4 kernels (32-bit accumulators, L <= 2) and the v4s
   // ones (64-bit accumulators, L <= 8)
-  const int lmax = v4_a32(ctx, q) ? 3 : 8;
+  const int lmax = v4_a32(ctx, q) ? 2 : 8;
   if (ctx->br_variant == 4 &&
       !(q.k == 2 && q.n <= v4::NMAX && q.pbs_level <= lmax && (q.pbs_level == 1 || q.pbs_base_log <= 16)))
     return 2;
@@ -1157,6 +1160,10 @@ static int launch_br_table(fhe_ctx* ctx, const uint64_t* d_small, int64_t count,
       const int npoly = (int)(fhe_bsk_words(&p) / p.N);
       hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, ctx->bsk, npoly, ctx->tw, ctx->twist,
                          ctx->bsk_fft_v2);
+      // once per key: a later table bootstrap on another stream must not
+      // read the copy before this conversion has finished
+      HIPCHK(ctx, hipGetLastError());
+      HIPCHK(ctx, hipStreamSynchronize(st));
     }
   }
   const c64* bsk = (p.N == 1024 && ctx->bsk_fft_v2) ? ctx->bsk_fft_v2 : ctx->bsk_fft;
@@ -1345,8 +1352,9 @@ static int sign_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uin
     if (!ctx->lane_st[l]) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->lane_st[l], hipStreamNonBlocking));
   for (int l = 0; l < 3; ++l)
     if (!ctx->lane_ev[l]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->lane_ev[l], hipEventDisableTiming));
-  int rc = ks_reserve(ctx, c0, 0);
-  if (!rc) rc = ks_reserve(ctx, c1, 1);
+  // the MFMA key switch's per-lane workspaces (the VALU variant needs none)
+  int rc = ctx->ks_variant == 2 ? ks_reserve(ctx, c0, 0) : FHE_OK;
+  if (!rc && ctx->ks_variant == 2) rc = ks_reserve(ctx, c1, 1);
   if (rc) return rc;
   HIPCHK(ctx, hipEventRecord(ctx->lane_ev[0], st));
   for (int l = 0; l < 2; ++l) HIPCHK(ctx, hipStreamWaitEvent(ctx->lane_st[l], ctx->lane_ev[0], 0));
@@ -1414,6 +1422,32 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   rc = sign_extract_batch(ctx, ctv, B, sgn, small, st);
   if (rc) return rc;
   rc = fhe_decrypt_bits_batch(ctx, sgn, B, d_below, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+// The reference's own encrypted predict (fhe_similarity.py:142-160): the
+// leveled circuit only. No key switch and no bootstrap; T only centres the
+// accumulator in the msg_bits-bit encoding (acc - T must fit it).
+int fhe_score_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                    int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_acc))) return fail(ctx, FHE_E_ARG, "bad score arguments");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t Wb = fhe_big_lwe_words(&p);
+  // workspace: ct_v (B big) | v (B)
+  rc = ensure_ws(ctx, 8 * ((size_t)B * Wb + (size_t)B));
+  if (rc) return rc;
+  u64* ctv = (u64*)ctx->ws;
+  int64_t* v = (int64_t*)(ctv + (size_t)B * Wb);
+  rc = fhe_encrypt_linear_batch(ctx, d_qx, B, D, enc_seed, id0, d_w, cst - T, ctv, stream);
+  if (rc) return rc;
+  rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
   HIPCHK(ctx, hipGetLastError());

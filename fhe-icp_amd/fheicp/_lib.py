@@ -74,6 +74,7 @@ SIGNATURES = [
     ("fhe_pbs_table_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _i32, _vp, _vp]),
     ("fhe_threshold_batch", C.c_int, [_CTXP, _vp, _i64, _i64, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
+    ("fhe_score_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp]),
     ("fhe_encrypt_seeded_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("fhe_expand_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     ("fhe_linear_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp, _vp]),

@@ -235,6 +235,16 @@ class Engine:
                                             _stream(self.device)))
         return acc, below
 
+    def score(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc_seed: int, id0: int = 0):
+        """The leveled circuit alone (fhe_score_batch): encrypt -> linear ->
+        decrypt, no key switch or bootstrap. T centres acc in the encoding.
+        Returns acc int64[B]."""
+        B, D = q_x.shape
+        acc = torch.empty(B, dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_score_batch(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T),
+                                          C.c_uint64(enc_seed), C.c_uint64(id0), _ptr(acc), _stream(self.device)))
+        return acc
+
     # ------------------------------------------- seeded (stored) corpus --
     @staticmethod
     def key_from_seed(seed: int) -> np.ndarray:

@@ -183,20 +183,37 @@ class FheLinearModel:
         T = min(max(int(T), lo), hi + 1)
         return self.engine.compare(qx_dev, self._w_dev, self.qparams.cst, T, self.enc_seed, self.next_id0(B * qx_dev.shape[1]))
 
+    def encrypted_score(self, qx_dev):
+        """The reference's encrypted predict as it is (fhe_similarity.py:142-160):
+        the leveled circuit only (fhe_score_batch, no PBS). Returns acc int64[B]
+        (device)."""
+        if self.engine is None:
+            raise RuntimeError("Model not compiled. Call compile() first.")
+        B = qx_dev.shape[0]
+        lo, hi = self.qparams.acc_range()
+        centre = (lo + hi) // 2      # |acc - centre| <= (hi - lo) / 2 + 1 fits msg_bits
+        return self.engine.score(qx_dev, self._w_dev, self.qparams.cst, centre, self.enc_seed,
+                                 self.next_id0(B * qx_dev.shape[1]))
+
     def predict_encrypted(self, X, threshold: float | None = None):
         """Encrypted predict for features X [B, D] (numpy). Returns float64
         scores and, if a threshold is given, below[b] = score < threshold
-        decided under encryption (else zeros)."""
+        decided under encryption by the bootstrapped sign extraction. Without
+        a threshold only the leveled circuit runs (no key switch or bootstrap),
+        as in the reference, and below is all zeros."""
         import torch
         X = np.asarray(X)
         if X.ndim == 1:
             X = X.reshape(1, -1)
         Xd = torch.from_numpy(np.ascontiguousarray(X)).to(self.engine.device)
         qx = self.quantize_dev(Xd)
-        T = threshold_int(self.qparams, threshold) if threshold is not None else 0
-        acc, below = self.encrypted_acc(qx, T)
+        if threshold is None:
+            acc = self.encrypted_score(qx)
+            below = None
+        else:
+            acc, below = self.encrypted_acc(qx, threshold_int(self.qparams, threshold))
         scores = np.float64(self.qparams.out_scale) * acc.cpu().numpy().astype(np.float64)
-        b = below.cpu().numpy() if threshold is not None else np.zeros(len(scores), np.int64)
+        b = below.cpu().numpy() if below is not None else np.zeros(len(scores), np.int64)
         return scores, b
 
     def clear_acc(self, X) -> np.ndarray:

@@ -7,7 +7,7 @@ This file format makes a model reproducible across processes and GPUs
 (SURVEY.md §8f-2):
 
     npz (no pickles; load with allow_pickle=False), mode 0600
-      meta     uint8[]  UTF-8 JSON {"format": "fheicp-model", "version": 1,
+      meta     uint8[]  UTF-8 JSON {"format": "fheicp-model", "version": 2,
                         "quant": QuantParams.to_dict(), "scheme": SchemeParams,
                         "secret": {"kdf": "pbkdf2-sha256", "iterations", "salt",
                                    "bits": {"s_small": n, "s_big": kN}}}
@@ -21,6 +21,9 @@ This file format makes a model reproducible across processes and GPUs
 The password comes from ``password=`` or ``$FHE_MASTER_PASSWORD``; without
 one, saving secret keys raises unless ``allow_plaintext_secrets=True`` (then
 s_small / s_big are stored as plain uint64 arrays, as version-1 files did).
+Version 2 is the format with the Fernet-wrapped ``secret`` blob; version-1
+files (plaintext s_small / s_big) still load. ``load_model(..., keys=False)``
+reads only the quantisation and scheme (the clear modes need no secret).
 """
 from __future__ import annotations
 
@@ -35,7 +38,7 @@ from .model import QuantParams
 from .params import SchemeParams
 
 FORMAT = "fheicp-model"
-VERSION = 1
+VERSION = 2                 # 2: Fernet-wrapped "secret" blob; 1: plaintext secret keys
 KEY_NAMES = ("s_small", "s_big", "bsk", "ksk")
 SECRET_NAMES = ("s_small", "s_big")
 KDF_ITERATIONS = 100_000
@@ -110,23 +113,32 @@ def save_model(path: str, qparams: QuantParams, scheme: SchemeParams, keys: dict
     _write_private(path, arrays)
 
 
-def load_model(path: str, password: str | None = None):
-    """-> (QuantParams, SchemeParams, keys dict or None)."""
+def _check_version(path: str, meta: dict, supported: int) -> None:
+    v = int(meta.get("version", 0))
+    if not 1 <= v <= supported:
+        raise ValueError(f"{path}: format version {meta.get('version')} is not supported (1..{supported})")
+    if v == 1 and "secret" in meta:
+        raise ValueError(f"{path}: version-1 file with an encrypted secret blob (corrupt)")
+
+
+def load_model(path: str, password: str | None = None, keys: bool = True):
+    """-> (QuantParams, SchemeParams, keys dict or None). keys=False skips the
+    key material (and so needs no password)."""
+    want_keys = keys
     with np.load(path, allow_pickle=False) as z:
         meta = json.loads(bytes(z["meta"]).decode())
         if meta.get("format") != FORMAT:
             raise ValueError(f"{path}: not an {FORMAT} file")
-        if int(meta.get("version", 0)) > VERSION:
-            raise ValueError(f"{path}: format version {meta['version']} is newer than supported {VERSION}")
+        _check_version(path, meta, VERSION)
         keys = None
-        if "bsk" in z.files and "ksk" in z.files:
+        if want_keys and "bsk" in z.files and "ksk" in z.files:
             keys = {"bsk": z["bsk"].copy(), "ksk": z["ksk"].copy()}
             keys.update(_read_secrets(z, meta, password, path))
     return QuantParams.from_dict(meta["quant"]), SchemeParams(**meta["scheme"]), keys
 
 
 CORPUS_FORMAT = "fheicp-corpus"
-CORPUS_VERSION = 1
+CORPUS_VERSION = 2          # as VERSION
 
 
 def save_corpus(path: str, corpus, password: str | None = None, allow_plaintext_secrets: bool = False) -> None:
@@ -154,8 +166,7 @@ def load_corpus(path: str, device: int = 0, password: str | None = None):
         meta = json.loads(bytes(z["meta"]).decode())
         if meta.get("format") != CORPUS_FORMAT:
             raise ValueError(f"{path}: not an {CORPUS_FORMAT} file")
-        if int(meta.get("version", 0)) > CORPUS_VERSION:
-            raise ValueError(f"{path}: format version {meta['version']} is newer than supported {CORPUS_VERSION}")
+        _check_version(path, meta, CORPUS_VERSION)
         keys = {"bsk": z["bsk"].copy(), "ksk": z["ksk"].copy()}
         keys.update(_read_secrets(z, meta, password, path))
     cq = CorpusQuant(QuantParams.from_dict(meta["quant"]), int(meta["corpus"]["n_e"]), float(meta["corpus"]["s_e"]))

@@ -47,8 +47,12 @@ class FheCircuit:
 
     @property
     def pbs_per_prediction(self) -> int:
-        """Key switches and bootstraps per encrypted prediction with a threshold."""
-        return self._model.msg_bits
+        """Key switches and bootstraps per encrypted prediction with a
+        threshold (predict_threshold: the sign extraction's schedule,
+        fhe_sign_pbs_count). predict(fhe="execute") itself runs none: it is
+        the reference's leveled circuit."""
+        from .params import sign_pbs_count
+        return sign_pbs_count(self._model.scheme)
 
 
 class LinearRegression:

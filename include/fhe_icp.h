@@ -237,6 +237,14 @@ int fhe_threshold_batch(fhe_ctx* ctx, const uint64_t* d_ct_acc, int64_t count, i
  * (fhe_encrypt_linear_batch), so D does not enter the footprint. */
 int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                       int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream);
+/* The reference's predict(fhe="execute") as it is (fhe_similarity.py:142-160,
+ * one row per call at :149-158): a leveled circuit with no PBS. encrypt q_x
+ * -> linear with d_w and cst - T -> decrypt; d_acc[b] = the accumulator
+ * (exact int64). No key switch or bootstrap runs; T only centres the value in
+ * the msg_bits-bit encoding (acc - T must fit it; the estimator passes the
+ * middle of the accumulator range). Workspace ~8 * B * (kN + 2) bytes. */
+int fhe_score_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                    int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, void* stream);
 
 /* ---- seeded (compressed) ciphertexts: the encrypted document corpus -------
  * Persisted documents (EncryptedDocument at

@@ -318,3 +318,61 @@ def test_processor_loads_persisted_model(tmp_path):
     persist.save_model(path, qp, p.fhe_model.model._fitted().scheme)
     p2 = _processor(tmp_path / "b", model_path=path, seed=999)   # a different seed would retrain differently
     assert p2.fhe_model.model.quant_params.to_dict() == qp.to_dict()
+
+
+def test_clear_processor_loads_wrapped_model_without_password(tmp_path, monkeypatch):
+    """The clear modes read only the quantisation of a model_path file, so a
+    file whose secret keys are Fernet-wrapped loads without a password
+    (persist.load_model(keys=False)); loading its keys still needs one."""
+    from fheicp import persist
+    monkeypatch.delenv("FHE_MASTER_PASSWORD", raising=False)
+    p = _processor(tmp_path / "a")
+    qp = p.fhe_model.model.quant_params
+    rng = np.random.default_rng(4)
+    keys = {"s_small": rng.integers(0, 2, 887).astype(np.uint64), "s_big": rng.integers(0, 2, 2048).astype(np.uint64),
+            "bsk": rng.integers(0, 2 ** 63, 8, dtype=np.uint64), "ksk": rng.integers(0, 2 ** 63, 8, dtype=np.uint64)}
+    path = str(tmp_path / "wrapped.npz")
+    persist.save_model(path, qp, p.fhe_model.model._fitted().scheme, keys, password="pw")
+    with pytest.raises(ValueError):
+        persist.load_model(path)
+    qp2, _, k = persist.load_model(path, keys=False)
+    assert k is None and qp2.to_dict() == qp.to_dict()
+    p2 = _processor(tmp_path / "b", model_path=path, seed=999)
+    assert p2.fhe_model.model.quant_params.to_dict() == qp.to_dict()
+
+
+def test_persist_versions(tmp_path):
+    """Files are written as version 2; version-1 files (plaintext secret keys)
+    still load; unknown versions are refused instead of read as key-less."""
+    import json
+    from fheicp import persist
+    from fheicp.params import params_for_bits
+    from fheicp.sklearn import LinearRegression
+    X, y = _data(16)
+    qp = LinearRegression(n_bits=6).fit(X, y).quant_params
+    sch = params_for_bits(qp.msg_bits())
+    keys = {k: np.arange(6, dtype=np.uint64) % 2 for k in persist.KEY_NAMES}
+    path = str(tmp_path / "m.npz")
+    persist.save_model(path, qp, sch, keys, allow_plaintext_secrets=True)
+    with np.load(path) as z:
+        assert json.loads(bytes(z["meta"]).decode())["version"] == 2
+    for v, ok in ((1, True), (2, True), (3, False), (0, False)):
+        meta = {"format": persist.FORMAT, "version": v, "quant": qp.to_dict(), "scheme": sch.as_dict()}
+        arrays = {k: keys[k] for k in persist.KEY_NAMES}
+        arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+        np.savez(path, **arrays)
+        if ok:
+            _, _, k2 = persist.load_model(path)
+            for k in persist.KEY_NAMES:
+                np.testing.assert_array_equal(k2[k], keys[k])
+        else:
+            with pytest.raises(ValueError):
+                persist.load_model(path)
+
+
+def test_corpus_secret_checked_before_keygen(tmp_path, monkeypatch):
+    """A processor that will save an encrypted corpus refuses to start without
+    a password (or the plaintext opt-in) before any training or keygen."""
+    monkeypatch.delenv("FHE_MASTER_PASSWORD", raising=False)
+    with pytest.raises(ValueError, match="password"):
+        _processor(tmp_path, fhe="execute", store_ciphertexts=True, corpus_path=str(tmp_path / "c.npz"))

@@ -39,6 +39,41 @@ def test_estimator_threshold_bit(fitted):
         np.testing.assert_array_equal(keep, clear >= t)
 
 
+def _br_totals(eng):
+    gs = ("main", "mid", "mid2", "fast", "fast2")
+    rd = {g: eng.profile_read(f"blind_rotate_{g}") for g in gs}
+    return (sum(r["launches"] for r in rd.values()), sum(r["items"] for r in rd.values()),
+            eng.profile_read("keyswitch")["launches"])
+
+
+def test_execute_is_leveled_only(fitted):
+    """predict(fhe="execute") is the reference's PBS-free leveled circuit
+    (fhe_similarity.py:142-160, fhe_score_batch): bit-exact scores, and no
+    key switch or blind rotation launches at all; predict_threshold runs the
+    sign extraction, pbs_per_prediction bootstraps per compare (the count the
+    bench reports as pbs_per_compare)."""
+    from fheicp.params import sign_pbs_count
+    est, ref = fitted
+    eng = est._fitted().engine
+    q, docs = Q.make_corpus(16, 300, seed=17)
+    X = Q.pair_features(q, docs)
+    eng.profile(True)
+    got = est.predict(X, fhe="execute")
+    br_launches, _, ks_launches = _br_totals(eng)
+    eng.profile(False)
+    np.testing.assert_array_equal(got, Q.predict(ref, X))
+    assert br_launches == 0 and ks_launches == 0
+    assert est.fhe_circuit.pbs_per_prediction == sign_pbs_count(eng.params)
+    eng.profile(True)
+    scores, keep = est.predict_threshold(X, 0.5)
+    _, br_items, ks_launches = _br_totals(eng)
+    eng.profile(False)
+    np.testing.assert_array_equal(scores, Q.predict(ref, X))
+    np.testing.assert_array_equal(keep, Q.predict(ref, X) >= 0.5)
+    assert br_items == est.fhe_circuit.pbs_per_prediction * len(X)
+    assert ks_launches == est.fhe_circuit.pbs_per_prediction
+
+
 def test_similarity_model_encrypted_and_key_persistence(need_gpu, tmp_path, monkeypatch):
     from fhe_similarity import FHESimilarityModel
     monkeypatch.setenv("FHE_MASTER_PASSWORD", "persist-pw")   # wraps the secret keys (fheicp.persist)

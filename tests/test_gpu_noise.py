@@ -32,6 +32,8 @@ INSTANCES = {
     (14, 2, 1): "k_blind_rotate_v4<2, true, 0, 4, false, 0>",   # run-time base log
     (22, 1, 1): "k_blind_rotate_v4<1, true, 0, 4, false, 0>",
     (12, 3, 1): "k_blind_rotate_v4s<3, false, 0, 0>",
+    # level 3 with L * beta <= 31: the 64-bit kernel too (no 32-bit level-3 instance ships)
+    (10, 3, 1): "k_blind_rotate_v4s<3, false, 0, 0>",
     (10, 4, 1): "k_blind_rotate_v4s<4, false, 0, 0>",
     (8, 5, 1): "k_blind_rotate_v4s<5, false, 0, 0>",
     (7, 6, 1): "k_blind_rotate_v4s<6, false, 0, 0>",
