@@ -1,0 +1,649 @@
+// The embedding stage's encoder on gfx950 (include/fhe_bert.h, SURVEY.md
+// §8 f4): BertEmbedder.get_embeddings_batch
+// (bert_embeddings.py:103-158) from token ids to the pooled float32
+// embedding. Second translation unit of libfheicp.so.
+//
+// Layout in HBM: the residual stream h in fp32 [M][H] (M = B * S tokens) with
+// a bf16 copy hb feeding the GEMMs; weights bf16 in torch's [out][in] layout
+// (so both GEMM operands are K-contiguous: A = activations [M][K], B^T =
+// W [N][K]); Q, K and V of a layer come out of ONE GEMM against the stacked
+// [3H][H] weight. Per layer: QKV GEMM -> fused attention -> output GEMM with
+// the residual add fused -> LayerNorm -> FFN GEMM with GELU fused -> FFN
+// output GEMM with the residual fused -> LayerNorm.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fhe_bert.h"
+#include "../../include/fhe_icp.h"
+
+namespace fbert {
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- GEMM: out[M][N] = A[M][K] . W[N][K]^T + bias (+ epilogue) ------------
+// 128 x 128 block tile, K step 64, 4 waves in 2 x 2, each a 64 x 64 tile of
+// 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators. Operands go global -> registers
+// -> LDS (double buffered, one barrier per K step); LDS rows are padded to 72
+// bf16 (144 B = 9 x 16 B), so the 16 lanes of a ds_read_b128 group (rows
+// l & 15) land on 16 distinct bank quads (9 r mod 16 is a permutation).
+constexpr int BM = 128, BN = 128, BK = 64, LDK = BK + 8;
+constexpr int GEMM_LDS = 2 * (BM + BN) * LDK * (int)sizeof(bf16);  // 73728 B
+enum { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2 };
+
+template <int EPI>
+__global__ void __launch_bounds__(256) k_gemm(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                              const float* __restrict__ bias, const float* __restrict__ resid,
+                                              void* __restrict__ out, int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* sa = reinterpret_cast<bf16*>(smem);   // [2][BM][LDK]
+  bf16* sb = sa + 2 * BM * LDK;               // [2][BN][LDK]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int KT = K / BK;
+  uint4 ra[4], rb[4];
+  auto load_regs = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, kc = (c & 7) * 8;
+      const int gm = m0 + row, gn = n0 + row, k = kt * BK + kc;
+      ra[i] = gm < M ? *reinterpret_cast<const uint4*>(A + (size_t)gm * K + k) : make_uint4(0, 0, 0, 0);
+      rb[i] = gn < N ? *reinterpret_cast<const uint4*>(W + (size_t)gn * K + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_lds = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 3, kc = (c & 7) * 8;
+      *reinterpret_cast<uint4*>(sa + (buf * BM + row) * LDK + kc) = ra[i];
+      *reinterpret_cast<uint4*>(sb + (buf * BN + row) * LDK + kc) = rb[i];
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load_regs(0);
+  store_lds(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_regs(kt + 1);  // in flight during the MFMAs
+    const bf16* ca = sa + (cur * BM + wm * 64 + (l & 15)) * LDK + 8 * (l >> 4);
+    const bf16* cb = sb + (cur * BN + wn * 64 + (l & 15)) * LDK + 8 * (l >> 4);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ca + 16 * i * LDK + 32 * ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(cb + 16 * j * LDK + 32 * ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    // the other buffer was last read before the previous barrier
+    if (kt + 1 < KT) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+  // C/D of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + 16 * j + (l & 15);
+    if (col >= N) continue;
+    const float bv = bias[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + 16 * i + 4 * (l >> 4) + r;
+        if (row >= M) continue;
+        float v = acc[i][j][r] + bv;
+        const size_t o = (size_t)row * N + col;
+        if constexpr (EPI == EPI_RESID_F32) {
+          reinterpret_cast<float*>(out)[o] = v + resid[o];
+        } else {
+          if constexpr (EPI == EPI_GELU_BF16) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+          reinterpret_cast<bf16*>(out)[o] = (bf16)v;
+        }
+      }
+  }
+}
+
+// ---- fused attention (flash-style) ------------------------------------------
+// One workgroup per (sequence, head) and 64 query rows; 4 waves of 16 rows.
+// K ([Sp][72]) and V transposed ([64][Sp + 8]) of the head are staged in LDS
+// once; each wave walks the keys in chunks of 64: S = Q K^T by MFMA (scale
+// 1/8, key mask as -inf), online softmax (running max and sum per row), P
+// (bf16) through a wave-private LDS tile into the A operand of O += P V.
+// Rows: 4 (lane >> 4) + reg of the 16x16 C layout, so a row's 16 keys of a
+// tile sit on the 16 lanes of one lane group (xor-shuffle reductions).
+constexpr int HD = 64, KLD = HD + 8;
+
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) k_attention(const bf16* __restrict__ qkv, const int32_t* __restrict__ mask,
+                                                   bf16* __restrict__ ctx, int S, int Sp, int nh, int H) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int VLD = Sp + 8;
+  bf16* Ks = reinterpret_cast<bf16*>(smem);       // [Sp][KLD]
+  bf16* Vt = Ks + Sp * KLD;                        // [HD][VLD]
+  bf16* Ps = Vt + HD * VLD;                        // [4][16][KLD]
+  float* madd = reinterpret_cast<float*>(Ps + 4 * 16 * KLD);  // [Sp]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x / nh, h = blockIdx.x - b * nh;
+  const int H3 = 3 * H;
+  const bf16* base = qkv + (size_t)b * S * H3 + h * HD;
+  for (int idx = tid; idx < Sp * 8; idx += 256) {
+    const int s = idx >> 3, c = (idx & 7) * 8;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (s < S) {
+      kv = *reinterpret_cast<const uint4*>(base + (size_t)s * H3 + H + c);
+      vv = *reinterpret_cast<const uint4*>(base + (size_t)s * H3 + 2 * H + c);
+    }
+    *reinterpret_cast<uint4*>(Ks + s * KLD + c) = kv;
+    const bf16* ve = reinterpret_cast<const bf16*>(&vv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Vt[(c + j) * VLD + s] = ve[j];
+  }
+  for (int s = tid; s < Sp; s += 256) madd[s] = (s < S && mask[(size_t)b * S + s] != 0) ? 0.0f : -INFINITY;
+  __syncthreads();
+  const int q0 = blockIdx.y * 64 + w * 16;
+  if (q0 >= S) return;  // no barrier below
+  const int qr = q0 + (l & 15);
+  bf16x8 qa[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint4 z = qr < S ? *reinterpret_cast<const uint4*>(base + (size_t)qr * H3 + 32 * ks + 8 * (l >> 4))
+                           : make_uint4(0, 0, 0, 0);
+    qa[ks] = __builtin_bit_cast(bf16x8, z);
+  }
+  float m[4], lsum[4];
+  f32x4 o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) m[r] = -INFINITY, lsum[r] = 0.0f;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16* pw = Ps + w * 16 * KLD;
+  for (int c0 = 0; c0 < Sp; c0 += 64) {
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const bf16* kr = Ks + (c0 + 16 * t + (l & 15)) * KLD + 8 * (l >> 4);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], *reinterpret_cast<const bf16x8*>(kr + 32 * ks), s[t], 0,
+                                                       0, 0);
+      const float ma = madd[c0 + 16 * t + (l & 15)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[t][r] = s[t][r] * 0.125f + ma;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mc = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+      mc = group16_max(mc);
+      const float mn = fmaxf(m[r], mc);
+      // chunk 0 holds key 0 ([CLS], never masked), so mn is finite from it on
+      const float alpha = __expf(m[r] - mn);
+      m[r] = mn;
+      float ps = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float p = __expf(s[t][r] - mn);
+        s[t][r] = p;
+        ps += p;
+      }
+      lsum[r] = lsum[r] * alpha + ps;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d][r] *= alpha;
+    }
+    // P -> the wave's LDS tile (rows 4 (l >> 4) + r, keys 16 t + (l & 15)),
+    // read back as A fragments; one wave's DS operations complete in order
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pw[(4 * (l >> 4) + r) * KLD + 16 * t + (l & 15)] = (bf16)s[t][r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(pw + (l & 15) * KLD + 32 * ks + 8 * (l >> 4));
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8 vb =
+            *reinterpret_cast<const bf16x8*>(Vt + (16 * d + (l & 15)) * VLD + c0 + 32 * ks + 8 * (l >> 4));
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[d], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next chunk's P writes follow these reads
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float inv = 1.0f / group16_sum(lsum[r]);
+    const int row = q0 + 4 * (l >> 4) + r;
+    if (row >= S) continue;
+    bf16* dst = ctx + ((size_t)b * S + row) * H + h * HD + (l & 15);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dst[16 * d] = (bf16)(o[d][r] * inv);
+  }
+}
+
+// ---- LayerNorm, embeddings, pooling ------------------------------------------
+// one wave per row of H <= 1024 (H / 64 values per lane), fp32 two-pass
+// mean / variance as torch.nn.functional.layer_norm (biased variance)
+constexpr int LN_MAXV = 16;
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ void ln_row(float (&v)[LN_MAXV], int nv, const float* g, const float* be, float eps,
+                                       int l, float* y, bf16* yb, int H) {
+  float s = 0.0f;
+  for (int j = 0; j < nv; ++j) s += v[j];
+  const float mean = wave_sum(s) / (float)H;
+  float q = 0.0f;
+  for (int j = 0; j < nv; ++j) {
+    const float d = v[j] - mean;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)H + eps);
+  for (int j = 0; j < nv; ++j) {
+    const int c = j * 64 + l;
+    const float r = (v[j] - mean) * rstd * g[c] + be[c];
+    y[c] = r;
+    yb[c] = (bf16)r;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, const float* __restrict__ g,
+                                                   const float* __restrict__ be, float* __restrict__ y,
+                                                   bf16* __restrict__ yb, int M, int H, float eps) {
+  const int l = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = H / 64;
+  float v[LN_MAXV];
+  for (int j = 0; j < nv; ++j) v[j] = x[(size_t)row * H + j * 64 + l];
+  ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb + (size_t)row * H, H);
+}
+
+__global__ void __launch_bounds__(256) k_embed_ln(const int32_t* __restrict__ ids, const int32_t* __restrict__ tt,
+                                                  const float* __restrict__ we, const float* __restrict__ pe,
+                                                  const float* __restrict__ te, const float* __restrict__ g,
+                                                  const float* __restrict__ be, float* __restrict__ y,
+                                                  bf16* __restrict__ yb, int M, int S, int H, int vocab, int ntype,
+                                                  float eps) {
+  const int l = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int s = row % S;
+  int id = ids[row], t = tt ? tt[row] : 0;
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // the host checks the range; never read out of bounds
+  t = t < 0 ? 0 : (t >= ntype ? ntype - 1 : t);
+  const int nv = H / 64;
+  float v[LN_MAXV];
+  for (int j = 0; j < nv; ++j) {
+    const int c = j * 64 + l;
+    v[j] = we[(size_t)id * H + c] + te[(size_t)t * H + c] + pe[(size_t)s * H + c];
+  }
+  ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb + (size_t)row * H, H);
+}
+
+// bert_embeddings.py:140-149: mean over the attention mask, [CLS], or max over
+// all S positions; thread per (sequence, feature)
+__global__ void k_pool(const float* __restrict__ h, const int32_t* __restrict__ mask, float* __restrict__ out, int B,
+                       int S, int H, int mode) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * H) return;
+  const int b = (int)(e / H), c = (int)(e - (int64_t)b * H);
+  const float* hb = h + (size_t)b * S * H + c;
+  float r;
+  if (mode == FHE_BERT_POOL_CLS) {
+    r = hb[0];
+  } else if (mode == FHE_BERT_POOL_MAX) {
+    r = hb[0];
+    for (int s = 1; s < S; ++s) r = fmaxf(r, hb[(size_t)s * H]);
+  } else {
+    float sum = 0.0f, cnt = 0.0f;
+    for (int s = 0; s < S; ++s) {
+      const float mk = (float)mask[(size_t)b * S + s];
+      sum += hb[(size_t)s * H] * mk;
+      cnt += mk;
+    }
+    r = sum / cnt;
+  }
+  out[e] = r;
+}
+}  // namespace fbert
+
+// ================================================================ host ======
+using namespace fbert;
+
+namespace {
+struct Layer {
+  bf16 *wqkv = nullptr, *wo = nullptr, *wi = nullptr, *wo2 = nullptr;
+  float *bqkv = nullptr, *bo = nullptr, *bi = nullptr, *bo2 = nullptr;
+  float *ln1w = nullptr, *ln1b = nullptr, *ln2w = nullptr, *ln2b = nullptr;
+};
+struct Prof {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  int64_t launches = 0;
+  double flops = 0.0;
+};
+}  // namespace
+
+struct fhe_bert {
+  fhe_bert_config cfg{};
+  int device = -1;
+  std::string err;
+  float *we = nullptr, *pe = nullptr, *te = nullptr, *elnw = nullptr, *elnb = nullptr;
+  std::vector<Layer> layers;
+  std::vector<uint64_t> have;  // bit set of tensors loaded, per layer (+1 for the embeddings)
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  bool prof = false;
+  Prof p_gemm, p_attn, p_other;
+};
+
+static int bfail(fhe_bert* h, int code, const std::string& m) {
+  if (h) h->err = m;
+  return code;
+}
+#define BCHK(h, call)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) return bfail(h, FHE_E_DEVICE, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static uint16_t to_bf16_bits(float f) {  // round to nearest even (finite inputs)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// (the entry points keep the C linkage of their declarations in fhe_bert.h)
+int fhe_bert_create(const fhe_bert_config* c, int device, fhe_bert** out) {
+  if (!c || !out) return FHE_E_ARG;
+  *out = nullptr;
+  if (c->hidden_size <= 0 || c->hidden_size % 64 || c->hidden_size > 64 * LN_MAXV || c->num_heads <= 0 ||
+      c->hidden_size != 64 * c->num_heads || c->intermediate_size <= 0 || c->intermediate_size % 64 ||
+      c->num_layers <= 0 || c->vocab_size <= 0 || c->max_position <= 0 || c->max_position > 512 ||
+      c->type_vocab_size <= 0 || !(c->layer_norm_eps > 0.0f))
+    return FHE_E_ARG;  // head dim 64, hidden <= 1024, S <= 512 (attention LDS)
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return FHE_E_DEVICE;
+  fhe_bert* h = new fhe_bert();
+  h->cfg = *c;
+  h->device = device;
+  h->layers.resize(c->num_layers);
+  h->have.assign(c->num_layers + 1, 0);
+  *out = h;
+  return FHE_OK;
+}
+
+static void free_all(fhe_bert* h) {
+  auto f = [](void* p) {
+    if (p) (void)hipFree(p);
+  };
+  f(h->we), f(h->pe), f(h->te), f(h->elnw), f(h->elnb), f(h->ws);
+  for (auto& L : h->layers) {
+    f(L.wqkv), f(L.wo), f(L.wi), f(L.wo2), f(L.bqkv), f(L.bo), f(L.bi), f(L.bo2);
+    f(L.ln1w), f(L.ln1b), f(L.ln2w), f(L.ln2b);
+  }
+  for (Prof* p : {&h->p_gemm, &h->p_attn, &h->p_other})
+    for (auto& e : p->ev) (void)hipEventDestroy(e.first), (void)hipEventDestroy(e.second);
+}
+
+void fhe_bert_destroy(fhe_bert* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  free_all(h);
+  delete h;
+}
+
+const char* fhe_bert_last_error(const fhe_bert* h) { return h ? h->err.c_str() : "null handle"; }
+
+template <class T>
+static int upload(fhe_bert* h, T** dst, const void* src, size_t bytes) {
+  if (!*dst) BCHK(h, hipMalloc((void**)dst, bytes));
+  BCHK(h, hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return FHE_OK;
+}
+
+int fhe_bert_set_tensor(fhe_bert* h, int32_t layer, int32_t which, const float* data, int64_t count) {
+  if (!h) return FHE_E_ARG;
+  if (!data || count <= 0) return bfail(h, FHE_E_ARG, "no data");
+  BCHK(h, hipSetDevice(h->device));
+  const fhe_bert_config& c = h->cfg;
+  const int64_t H = c.hidden_size, I = c.intermediate_size;
+  auto want = [&](int64_t n) { return count == n ? FHE_OK : bfail(h, FHE_E_ARG, "tensor " + std::to_string(which) +
+                                                                           ": expected " + std::to_string(n) +
+                                                                           " elements, got " + std::to_string(count)); };
+  int rc;
+  if (layer < 0) {
+    switch (which) {
+      case FHE_BERT_WORD_EMB: if ((rc = want((int64_t)c.vocab_size * H))) return rc; rc = upload(h, &h->we, data, count * 4); break;
+      case FHE_BERT_POS_EMB: if ((rc = want((int64_t)c.max_position * H))) return rc; rc = upload(h, &h->pe, data, count * 4); break;
+      case FHE_BERT_TYPE_EMB: if ((rc = want((int64_t)c.type_vocab_size * H))) return rc; rc = upload(h, &h->te, data, count * 4); break;
+      case FHE_BERT_EMB_LN_W: if ((rc = want(H))) return rc; rc = upload(h, &h->elnw, data, count * 4); break;
+      case FHE_BERT_EMB_LN_B: if ((rc = want(H))) return rc; rc = upload(h, &h->elnb, data, count * 4); break;
+      default: return bfail(h, FHE_E_ARG, "unknown embedding tensor id");
+    }
+    if (rc) return rc;
+    h->have[c.num_layers] |= 1ull << which;
+    return FHE_OK;
+  }
+  if (layer >= c.num_layers) return bfail(h, FHE_E_ARG, "layer out of range");
+  Layer& L = h->layers[layer];
+  // GEMM weights -> bf16; Q, K and V stack into one [3H][H] matrix
+  auto put_bf16 = [&](bf16** dst, size_t total, size_t off, int64_t n) -> int {
+    if ((rc = want(n))) return rc;
+    std::vector<uint16_t> t((size_t)n);
+    for (int64_t i = 0; i < n; ++i) t[(size_t)i] = to_bf16_bits(data[i]);
+    if (!*dst) BCHK(h, hipMalloc((void**)dst, total * 2));
+    BCHK(h, hipMemcpy(*dst + off, t.data(), (size_t)n * 2, hipMemcpyHostToDevice));
+    return FHE_OK;
+  };
+  auto put_f32 = [&](float** dst, size_t total, size_t off, int64_t n) -> int {
+    if ((rc = want(n))) return rc;
+    if (!*dst) BCHK(h, hipMalloc((void**)dst, total * 4));
+    BCHK(h, hipMemcpy(*dst + off, data, (size_t)n * 4, hipMemcpyHostToDevice));
+    return FHE_OK;
+  };
+  switch (which) {
+    case FHE_BERT_Q_W: rc = put_bf16(&L.wqkv, 3 * H * H, 0, H * H); break;
+    case FHE_BERT_K_W: rc = put_bf16(&L.wqkv, 3 * H * H, H * H, H * H); break;
+    case FHE_BERT_V_W: rc = put_bf16(&L.wqkv, 3 * H * H, 2 * H * H, H * H); break;
+    case FHE_BERT_Q_B: rc = put_f32(&L.bqkv, 3 * H, 0, H); break;
+    case FHE_BERT_K_B: rc = put_f32(&L.bqkv, 3 * H, H, H); break;
+    case FHE_BERT_V_B: rc = put_f32(&L.bqkv, 3 * H, 2 * H, H); break;
+    case FHE_BERT_AO_W: rc = put_bf16(&L.wo, H * H, 0, H * H); break;
+    case FHE_BERT_AO_B: rc = put_f32(&L.bo, H, 0, H); break;
+    case FHE_BERT_AO_LN_W: rc = put_f32(&L.ln1w, H, 0, H); break;
+    case FHE_BERT_AO_LN_B: rc = put_f32(&L.ln1b, H, 0, H); break;
+    case FHE_BERT_I_W: rc = put_bf16(&L.wi, I * H, 0, I * H); break;
+    case FHE_BERT_I_B: rc = put_f32(&L.bi, I, 0, I); break;
+    case FHE_BERT_O_W: rc = put_bf16(&L.wo2, H * I, 0, H * I); break;
+    case FHE_BERT_O_B: rc = put_f32(&L.bo2, H, 0, H); break;
+    case FHE_BERT_O_LN_W: rc = put_f32(&L.ln2w, H, 0, H); break;
+    case FHE_BERT_O_LN_B: rc = put_f32(&L.ln2b, H, 0, H); break;
+    default: return bfail(h, FHE_E_ARG, "unknown layer tensor id");
+  }
+  if (rc) return rc;
+  h->have[layer] |= 1ull << which;
+  return FHE_OK;
+}
+
+int fhe_bert_ready(const fhe_bert* h) {
+  if (!h) return 0;
+  const uint64_t emb = (1ull << 5) - 1, lay = ((1ull << 16) - 1) << 16;
+  if ((h->have[h->cfg.num_layers] & emb) != emb) return 0;
+  for (int l = 0; l < h->cfg.num_layers; ++l)
+    if ((h->have[l] & lay) != lay) return 0;
+  return 1;
+}
+
+int fhe_bert_profile_enable(fhe_bert* h, int enable) {
+  if (!h) return FHE_E_ARG;
+  h->prof = enable != 0;
+  return FHE_OK;
+}
+
+static void pbegin(fhe_bert* h, Prof& p, hipStream_t st, hipEvent_t* e1) {
+  *e1 = nullptr;
+  if (!h->prof) return;
+  hipEvent_t e0;
+  if (hipEventCreate(&e0) != hipSuccess) return;
+  if (hipEventCreate(e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    *e1 = nullptr;
+    return;
+  }
+  (void)hipEventRecord(e0, st);
+  p.ev.push_back({e0, *e1});
+}
+static void pend(fhe_bert* h, Prof& p, hipStream_t st, hipEvent_t e1, double flops) {
+  if (!h->prof || !e1) return;
+  (void)hipEventRecord(e1, st);
+  p.launches += 1;
+  p.flops += flops;
+}
+
+int fhe_bert_profile_read(fhe_bert* h, const char* kernel, double* total_ms, int64_t* launches, double* flops) {
+  if (!h || !kernel) return FHE_E_ARG;
+  Prof* p = !strcmp(kernel, "gemm") ? &h->p_gemm : !strcmp(kernel, "attention") ? &h->p_attn
+                                                    : !strcmp(kernel, "other") ? &h->p_other : nullptr;
+  if (!p) return bfail(h, FHE_E_ARG, "unknown kernel class");
+  double ms = 0.0;
+  for (auto& e : p->ev) {
+    BCHK(h, hipEventSynchronize(e.second));
+    float t = 0.0f;
+    BCHK(h, hipEventElapsedTime(&t, e.first, e.second));
+    ms += t;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  p->ev.clear();
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = p->launches;
+  if (flops) *flops = p->flops;
+  p->launches = 0;
+  p->flops = 0.0;
+  return FHE_OK;
+}
+
+template <int EPI>
+static int gemm(fhe_bert* h, const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M,
+                int N, int K, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    BCHK(h, hipFuncSetAttribute((const void*)k_gemm<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, GEMM_LDS));
+    attr = true;
+  }
+  hipEvent_t e1;
+  pbegin(h, h->p_gemm, st, &e1);
+  hipLaunchKernelGGL(k_gemm<EPI>, dim3((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM)), dim3(256),
+                     GEMM_LDS, st, A, W, bias, resid, out, M, N, K);
+  pend(h, h->p_gemm, st, e1, 2.0 * M * N * K);
+  BCHK(h, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, const int32_t* d_mask, int32_t B,
+                     int32_t S, int32_t pooling, float* d_out, void* stream) {
+  if (!h) return FHE_E_ARG;
+  const fhe_bert_config& c = h->cfg;
+  if (B < 0 || S < 1 || S > c.max_position || pooling < 0 || pooling > FHE_BERT_POOL_NONE ||
+      (B > 0 && (!d_ids || !d_mask || !d_out)))
+    return bfail(h, FHE_E_ARG, "bad forward arguments (1 <= S <= max_position)");
+  if (!fhe_bert_ready(h)) return bfail(h, FHE_E_STATE, "weights not loaded (fhe_bert_set_tensor)");
+  if (B == 0) return FHE_OK;
+  BCHK(h, hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int H = c.hidden_size, I = c.intermediate_size, nh = c.num_heads;
+  const int64_t M64 = (int64_t)B * S;
+  if (M64 > (1 << 24)) return bfail(h, FHE_E_ARG, "B * S too large: split the call");
+  const int M = (int)M64;
+  // workspace: h f32 | tmp f32 | hb bf16 | qkv bf16 | ctx bf16 | inter bf16
+  const size_t need = (size_t)M * (4 * H + 4 * H + 2 * H + 6 * H + 2 * H + 2 * I);
+  if (need > h->ws_bytes) {
+    if (h->ws) {
+      BCHK(h, hipDeviceSynchronize());
+      BCHK(h, hipFree(h->ws));
+      h->ws = nullptr;
+      h->ws_bytes = 0;
+    }
+    BCHK(h, hipMalloc(&h->ws, need));
+    h->ws_bytes = need;
+  }
+  float* hs = (float*)h->ws;
+  float* tmp = hs + (size_t)M * H;
+  bf16* hb = (bf16*)(tmp + (size_t)M * H);
+  bf16* qkv = hb + (size_t)M * H;
+  bf16* ctx = qkv + (size_t)M * 3 * H;
+  bf16* inter = ctx + (size_t)M * H;
+  const float eps = c.layer_norm_eps;
+  const unsigned rows4 = (unsigned)((M + 3) / 4);
+  hipEvent_t e1;
+  pbegin(h, h->p_other, st, &e1);
+  hipLaunchKernelGGL(k_embed_ln, dim3(rows4), dim3(256), 0, st, d_ids, d_type, h->we, h->pe, h->te, h->elnw, h->elnb,
+                     hs, hb, M, S, H, c.vocab_size, c.type_vocab_size, eps);
+  pend(h, h->p_other, st, e1, 0.0);
+  BCHK(h, hipGetLastError());
+  const int Sp = (S + 63) / 64 * 64;
+  const size_t attn_lds = (size_t)Sp * KLD * 2 + (size_t)HD * (Sp + 8) * 2 + 4 * 16 * KLD * 2 + (size_t)Sp * 4;
+  static bool attn_attr = false;
+  if (!attn_attr) {
+    BCHK(h, hipFuncSetAttribute((const void*)k_attention, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attn_attr = true;
+  }
+  int rc;
+  for (int li = 0; li < c.num_layers; ++li) {
+    const Layer& L = h->layers[li];
+    if ((rc = gemm<EPI_BF16>(h, hb, L.wqkv, L.bqkv, nullptr, qkv, M, 3 * H, H, st))) return rc;
+    pbegin(h, h->p_attn, st, &e1);
+    hipLaunchKernelGGL(k_attention, dim3((unsigned)(B * nh), (unsigned)(Sp / 64)), dim3(256), attn_lds, st, qkv,
+                       d_mask, ctx, S, Sp, nh, H);
+    pend(h, h->p_attn, st, e1, 4.0 * B * nh * (double)S * S * HD);
+    BCHK(h, hipGetLastError());
+    if ((rc = gemm<EPI_RESID_F32>(h, ctx, L.wo, L.bo, hs, tmp, M, H, H, st))) return rc;
+    pbegin(h, h->p_other, st, &e1);
+    hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps);
+    pend(h, h->p_other, st, e1, 0.0);
+    if ((rc = gemm<EPI_GELU_BF16>(h, hb, L.wi, L.bi, nullptr, inter, M, I, H, st))) return rc;
+    if ((rc = gemm<EPI_RESID_F32>(h, inter, L.wo2, L.bo2, hs, tmp, M, H, I, st))) return rc;
+    pbegin(h, h->p_other, st, &e1);
+    hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps);
+    pend(h, h->p_other, st, e1, 0.0);
+    BCHK(h, hipGetLastError());
+  }
+  if (pooling == FHE_BERT_POOL_NONE) {
+    BCHK(h, hipMemcpyAsync(d_out, hs, (size_t)M * H * 4, hipMemcpyDeviceToDevice, st));
+  } else {
+    const int64_t tot = (int64_t)B * H;
+    hipLaunchKernelGGL(k_pool, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, hs, d_mask, d_out, B, S, H,
+                       pooling);
+    BCHK(h, hipGetLastError());
+  }
+  return FHE_OK;
+}

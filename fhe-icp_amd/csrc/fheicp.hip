@@ -76,7 +76,7 @@ struct fhe_ctx {
   // fhe_compare_batch (created on first use)
   hipStream_t lane_st[2] = {nullptr, nullptr};
   hipEvent_t lane_ev[3] = {nullptr, nullptr, nullptr};
-  int ks_variant = 2;  // 2 = MFMA (default when ks_level == 4), 1 = VALU split-K
+  int ks_variant = 2;  // 2 = MFMA (i8 planes, any ks_level with kN % 64 == 0), 1 = VALU split-K
 };
 
 static std::mutex g_err_mu;
@@ -373,7 +373,12 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   if (const char* e = getenv("FHEICP_V4S")) ctx->v4s = atoi(e);
 #endif
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
-  if (params->ks_level != 4 || (params->k * params->N * 4) % 64 != 0) ctx->ks_variant = 1;
+  // the MFMA key switch: digits in i8, K = kN * ks_level level-major in
+  // 64-blocks, |sum| <= K * 2^(beta-1) * 128 < 2^31 in the i32 accumulators
+  if ((params->k * params->N) % 64 != 0 || params->ks_level * params->ks_base_log > 32 ||
+      params->ks_base_log > 8 ||
+      (double)params->k * params->N * params->ks_level * std::ldexp(1.0, params->ks_base_log - 1) * 128 >= 2147483648.0)
+    ctx->ks_variant = 1;
   // v4 covers k = 2, n <= 1023 at N = 1024; otherwise the two-wave kernel
   // (measured: v4 wins at gadget levels <= 3, e.g. 21.6 vs 23.6 ms at P=21; from
   // level 4 its 64-bit accumulator spills and v2 is faster, 40.6 vs 53.0 ms at P=26)
@@ -606,8 +611,8 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
     const int K = p.k * p.N * p.ks_level, n1 = p.n + 1, NB = (n1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
     if (!ctx->ksk8) HIPCHK(ctx, hipMalloc(&ctx->ksk8, (size_t)K * NB * 16 * 8));
     const int64_t tot = (int64_t)K * NB * 16;
-    hipLaunchKernelGGL(k_ksk_to_i8, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ctx->ksk, K, n1, NB,
-                       ctx->ksk8);
+    hipLaunchKernelGGL(k_ksk_to_i8, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ctx->ksk, K, p.k * p.N,
+                       p.ks_level, n1, NB, ctx->ksk8);
   }
   bsk_to_fft(ctx, p, ctx->bsk, ctx->bsk_fft, st);
   for (int g = 1; g < NGAD; ++g)
@@ -883,8 +888,8 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
     hipEvent_t e1;
     prof_begin(ctx, ctx->prof_ks, st, &e1);
     ctx->prof_ks.kernel = "k_keyswitch_mfma";
-    hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)KB, (unsigned)ncb), dim3(256), 0, st, d_big, count, p.k * p.N,
-                       p.ks_base_log, shift, add_body, KB, D, body);
+    hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)(p.k * p.N / 64), (unsigned)ncb), dim3(256), 0, st, d_big, count,
+                       p.k * p.N, p.ks_base_log, p.ks_level, shift, add_body, KB, D, body);
     hipLaunchKernelGGL(k_keyswitch_mfma, dim3((unsigned)((count + 63) / 64), (unsigned)NB), dim3(256), 0, st,
                        (const v4i*)D, (const v4i*)ctx->ksk8, body, count, n1, NB, KB, d_small);
     prof_end(ctx, ctx->prof_ks, st, e1, count);

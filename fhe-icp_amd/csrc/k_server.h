@@ -117,12 +117,16 @@ __global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, u64* 
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int KSM_NB_COLS = 16;  // columns per block
 
-// key planes: [kb][nb][q][lane][16 B]
-__global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int n1, int NB, int8_t* __restrict__ out) {
+// key planes: [kb][nb][q][lane][16 B]. The GEMM's K runs level-major,
+// k = l * big + i (a k-block of 64 is 64 consecutive input coefficients of
+// one level, for any ks_level); the KSK itself is stored [i][l][n+1].
+__global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int big, int levels, int n1, int NB,
+                            int8_t* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)K * NB * 16) return;
   const int row = (int)(e / (NB * 16)), col = (int)(e % (NB * 16));
-  u64 x = col < n1 ? ksk[(size_t)row * n1 + col] : 0;
+  const int l = row / big, i = row - l * big;
+  u64 x = col < n1 ? ksk[((size_t)i * levels + l) * n1 + col] : 0;
   const int kb = row >> 6, g = (row >> 4) & 3, j = row & 15;
   const int nb = col >> 4, lane = (col & 15) + 16 * g;
 #pragma unroll
@@ -133,28 +137,44 @@ __global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int n1, int NB, 
   }
 }
 
-// digits in A-fragment order [cb][kb][lane][16 B] (ks_level = 4: a
-// coefficient's 4 digits are 4 consecutive bytes) and b' = (b << shift) + add
+// digits in A-fragment order [cb][kb][lane][16 B] with K level-major (as
+// k_ksk_to_i8), and b' = (b << shift) + add_body. A thread takes 4
+// consecutive coefficients of one ciphertext and writes one packed word (4
+// digits, one byte each) per level; grid (big / 64, ceil(count / 16)), 256
+// threads: 16 ciphertexts x 64 coefficients. Needs big % 64 == 0,
+// levels <= 8 and levels * beta <= 32 (fhe_ctx_create).
 __global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, int64_t count, int big, int beta,
-                                                   int shift, u64 add_body, int KB, uint32_t* __restrict__ D,
-                                                   u64* __restrict__ body) {
-  const int t = threadIdx.x, cl = t >> 4, il = t & 15;
+                                                   int levels, int shift, u64 add_body, int KB,
+                                                   uint32_t* __restrict__ D, u64* __restrict__ body) {
+  const int t = threadIdx.x, cl = t >> 4, iq = t & 15;
   const int64_t cb = blockIdx.y, c = cb * 16 + cl;
-  const int kb = blockIdx.x, i = kb * 16 + il;
+  const int i0 = blockIdx.x * 64 + iq * 4;
   if (c >= count) return;
   const u64* src = in + (size_t)c * (big + 1);
-  if (kb == 0 && il == 0) body[c] = (src[big] << shift) + add_body;
-  const int prec = 4 * beta;
-  uint32_t r = (uint32_t)((((src[i] << shift) >> (63 - prec)) + 1) >> 1);
-  uint32_t packed = 0;
+  if (blockIdx.x == 0 && iq == 0) body[c] = (src[big] << shift) + add_body;
+  const int prec = levels * beta;
+  uint32_t packed[8];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {  // LSB-first; level l = 3 - s sits in byte l
-    const int d = __builtin_amdgcn_sbfe((int)r, s * beta, beta);
-    r -= (uint32_t)d << (s * beta);
-    packed |= (uint32_t)(uint8_t)(int8_t)d << (8 * (3 - s));
+  for (int s = 0; s < 8; ++s) packed[s] = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t r = (uint32_t)((((src[i0 + q] << shift) >> (63 - prec)) + 1) >> 1);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // LSB-first: digit s is level levels - 1 - s
+      if (s >= levels) break;
+      const int d = __builtin_amdgcn_sbfe((int)r, s * beta, beta);
+      r -= (uint32_t)d << (s * beta);
+      packed[s] |= (uint32_t)(uint8_t)(int8_t)d << (8 * q);
+    }
   }
-  const int lane = cl + 16 * (il >> 2);
-  D[(((size_t)cb * KB + kb) * 64 + lane) * 4 + (il & 3)] = packed;
+  const int lane = cl + 16 * ((i0 >> 4) & 3);
+  const int kbi = i0 >> 6, kbl = big >> 6;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    if (s >= levels) break;
+    const int kb = (levels - 1 - s) * kbl + kbi;
+    D[(((size_t)cb * KB + kb) * 64 + lane) * 4 + ((i0 & 15) >> 2)] = packed[s];
+  }
 }
 
 // workgroup = 4 waves = 64 ciphertexts x 16 columns x 8 byte planes; the key

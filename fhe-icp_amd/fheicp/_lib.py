@@ -94,6 +94,16 @@ SIGNATURES = [
     ("fhe_profile_read", C.c_int, [_CTXP, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64), C.POINTER(_i64)]),
     ("fhe_profile_kernel_name", C.c_int, [_CTXP, C.c_char_p, C.c_char_p, C.c_size_t]),
     ("fhe_build_info", C.c_char_p, []),
+    # include/fhe_bert.h: the embedding stage's encoder (fheicp.bert)
+    ("fhe_bert_create", C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
+    ("fhe_bert_destroy", None, [_vp]),
+    ("fhe_bert_last_error", C.c_char_p, [_vp]),
+    ("fhe_bert_set_tensor", C.c_int, [_vp, _i32, _i32, _vp, _i64]),
+    ("fhe_bert_ready", C.c_int, [_vp]),
+    ("fhe_bert_forward", C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),
+    ("fhe_bert_profile_enable", C.c_int, [_vp, C.c_int]),
+    ("fhe_bert_profile_read", C.c_int, [_vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64),
+                                        C.POINTER(C.c_double)]),
 ]
 
 _lib = None

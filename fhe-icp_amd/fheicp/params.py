@@ -24,8 +24,14 @@ class SchemeParams:
     N: int = 1024
     pbs_base_log: int = 15
     pbs_level: int = 2
-    ks_base_log: int = 4
-    ks_level: int = 4
+    # key switch: 5 levels of base 2^3 (15 bits). The modulus switch is the
+    # largest fixed noise term of a sign round (2^-8.39); the key switch
+    # comes next, and at (3, 5) it is 2^-10.72 against 2^-10.06 at (4, 4):
+    # enough margin that the P = 16 plan needs no classic main round (all
+    # multi-bit) and the P = 26 plan goes from 3- to 4-bit digits (17 -> 13
+    # bootstraps) for 1.25x the key-switch work
+    ks_base_log: int = 3
+    ks_level: int = 5
     lwe_noise_bits: int = 46
     glwe_noise_bits: int = 17
     msg_bits: int = 16

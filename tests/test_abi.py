@@ -10,12 +10,16 @@ import pytest
 from fheicp import _lib
 from fheicp.params import TOY, params_for_bits
 
-HEADER = Path(__file__).resolve().parents[1] / "include" / "fhe_icp.h"
+INCLUDE = Path(__file__).resolve().parents[1] / "include"
+HEADERS = sorted(INCLUDE.glob("*.h"))       # fhe_icp.h (the compare path), fhe_bert.h (§8 f4)
 
 
 def declared_functions():
-    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fhe_[a-z_0-9]+)\s*\(", text, flags=re.M)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fhe_[a-z_0-9]+)\s*\(", text, flags=re.M))
+    return sorted(names)
 
 
 def test_header_declares_expected_surface():
@@ -141,7 +145,7 @@ def test_mid_gadget_validation_and_schedule(oracle_lib):
     P = _lib.params_struct(base)
     R = L.fhe_sign_schedule(C.byref(P), None, 0)
     want = sign_schedule(params_for_bits(26))[1]
-    assert R == len(want) == 17
+    assert R == len(want) == 13
     out = (C.c_int32 * 4)(-1, -1, -1, -1)
     assert L.fhe_sign_schedule(C.byref(P), out, 3) == R and list(out) == want[:3] + [-1]
     ol = oracle_lib.lib()
@@ -153,3 +157,19 @@ def test_mid_gadget_validation_and_schedule(oracle_lib):
     buf = (C.c_uint64 * 1)()
     assert L.fhe_export_fast_bsk(h, 3, buf) == -2
     L.fhe_ctx_destroy(h)
+
+
+def test_bert_abi_validation():
+    """fhe_bert_create (include/fhe_bert.h) rejects configs the encoder does
+    not implement (head dim != 64, sequences beyond 512) and, on a host with
+    no device, fails with FHE_E_DEVICE instead of running anything."""
+    from fheicp.bert import BertConfigC
+    L = _lib.lib()
+    good = dict(vocab_size=30522, hidden_size=768, num_layers=12, num_heads=12, intermediate_size=3072,
+                max_position=512, type_vocab_size=2, layer_norm_eps=1e-12)
+    h = C.c_void_p()
+    for bad in (dict(good, num_heads=8), dict(good, max_position=1024), dict(good, hidden_size=770),
+                dict(good, intermediate_size=3000), dict(good, layer_norm_eps=0.0)):
+        assert L.fhe_bert_create(C.byref(BertConfigC(**bad)), 0, C.byref(h)) == -1, bad
+    assert L.fhe_bert_create(C.byref(BertConfigC(**good)), 0, C.byref(h)) == -2   # no GPU here
+    assert L.fhe_bert_ready(None) == 0

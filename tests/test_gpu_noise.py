@@ -89,3 +89,29 @@ def test_bootstrap_noise_vs_model(need_gpu, oracle_lib, gadget):
     assert np.abs(ph[:2] - ph_ref).max() < 8 * sigma_model * 2.0 ** 64
     assert np.array_equal(ph_ref > 0, sgn[:2] > 0)
     eng.close()
+
+
+@pytest.mark.parametrize("ks", [(3, 5), (4, 4)])
+def test_keyswitch_noise_vs_model(need_gpu, ks):
+    """The key switch's output noise (the second-largest fixed term of every
+    sign round after the modulus switch) against the model's
+    v_ks, for the shipped (3, 5) key switch (level-major i8 MFMA) and the
+    former (4, 4): 4096 fresh encryptions, switched, decrypted on the host
+    under the exported small key."""
+    from fheicp.params import params_for_bits
+    prm = replace(params_for_bits(16), ks_base_log=ks[0], ks_level=ks[1])
+    eng = Engine(prm, 0)
+    eng.keygen(6100 + ks[0])
+    rng = np.random.default_rng(ks[0])
+    v = rng.integers(-(2 ** 15), 2 ** 15, COUNT)
+    small = u64(eng.keyswitch(eng.encrypt(v, seed=23), 0, 0)).reshape(COUNT, prm.n + 1)
+    s = eng.export_keys()["s_small"].astype(np.uint64)
+    with np.errstate(over="ignore"):
+        ph = small[:, -1] - (small[:, :-1] * s[None, :]).sum(axis=1, dtype=np.uint64)
+    err = signed(ph - (v.astype(np.int64).astype(np.uint64) << np.uint64(64 - 16))).astype(np.float64) / 2.0 ** 64
+    sigma = float(np.sqrt(np.mean(err ** 2)))
+    sigma_model = math.sqrt(_variances(prm)[1])
+    print(f"key switch {ks}: sigma 2^{math.log2(sigma):.2f}, model 2^{math.log2(sigma_model):.2f}")
+    assert sigma <= 1.1 * sigma_model
+    assert sigma >= 0.7 * sigma_model        # the model is not vacuous either
+    eng.close()

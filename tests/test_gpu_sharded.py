@@ -56,7 +56,9 @@ def _rank_main(rank, world, port, store_dir, query, cases, q):
         res = [p.search_vector(np.asarray(query), k, t) for k, t in cases]
         torch.cuda.synchronize()
         eng.profile(False)
-        brs = {g: eng.profile_read(f"blind_rotate_{g}")["items"] for g in ("main", "fast", "fast2")}
+        brs = {g: eng.profile_read(f"blind_rotate_{g}")["items"] for g in ("main", "mid", "mid2", "fast", "fast2")}
+        from fheicp.params import sign_pbs_count
+        brs["per_compare"] = sign_pbs_count(eng.params)
         q.put((rank, res, p.fhe_model.model.quant_params.to_dict(), brs, _lib.LIB_PATH and str(_lib.LIB_PATH)))
         torch.distributed.destroy_process_group()
     except BaseException as e:  # report instead of hanging the parent on q.get
@@ -100,9 +102,11 @@ def test_processor_sharded_encrypted_search_two_ranks(need_gpu, tmp_path, monkey
     qp = Q.QuantizedLinearParams.from_json(res[0][2])
     for rank, got, qd, brs, lib in res:
         assert qd == res[0][2]
-        # the encrypted path ran: this rank bootstrapped its own range only
+        # the encrypted path ran: this rank bootstrapped its own range only,
+        # the sign extraction's bootstraps for each of its documents per case
         per_case = (301 if rank == 1 else 300)
-        assert sum(brs.values()) > 0 and brs["main"] == per_case * len(cases), brs
+        n_br = sum(v for g, v in brs.items() if g != "per_compare")
+        assert n_br == brs["per_compare"] * per_case * len(cases), brs
         assert lib and lib.endswith("libfheicp.so")
         for (k, t), g in zip(cases, got):
             want = [(ids[i], s) for i, s in Q.search(qp, qv, docs, k, t)]

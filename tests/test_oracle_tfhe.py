@@ -144,9 +144,9 @@ def test_sign_extract_digits_all_values(toy_ref, P, d):
 def test_sign_pbs_count(oracle_lib):
     from oracle.tfhe_ref import sign_pbs_count
     from fheicp.params import params_for_bits
-    # 4-bit digits where the noise bar allows them (P <= 21 here, with a more
+    # 4-bit digits where the noise bar allows them (P <= 26 here, with a more
     # precise main gadget from P = 17), else 3-bit
-    want = {1: 1, 2: 2, 3: 3, 4: 1, 6: 3, 7: 3, 8: 3, 9: 4, 16: 7, 17: 8, 21: 10, 26: 17}
+    want = {1: 1, 2: 2, 3: 3, 4: 1, 6: 3, 7: 3, 8: 3, 9: 4, 16: 7, 17: 8, 21: 10, 26: 13, 27: 17}
     assert {P: sign_pbs_count(params_for_bits(P).as_dict()) for P in want} == want
     want3 = {4: 2, 6: 3, 7: 4, 8: 5, 9: 5, 16: 10, 21: 13, 26: 17}
     got3 = {P: sign_pbs_count({**params_for_bits(P).as_dict(), "sign_digit_bits": 3}) for P in want3}

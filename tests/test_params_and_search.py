@@ -65,8 +65,9 @@ def test_sign_digits_match_oracle_and_library(oracle_lib):
         sched = (C.c_int32 * 64)()
         R = L.fhe_sign_schedule(cp, sched, 64)
         assert sign_schedule(p)[1] == oracle_lib.sign_schedule(d) == list(sched[:R]), d
-    # the headline width: 4-bit digits at P = 16, 3-bit where 4 misses the bar
-    assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 4, 4, 3]
+    # 4-bit digits at the configs' widths (with the (3, 5) key switch, C5's
+    # P = 26 too; it took 3-bit digits with the (4, 4) one)
+    assert [sign_digit_bits(params_for_bits(P)) for P in (16, 17, 21, 26)] == [4, 4, 4, 4]
     assert sign_pbs_count(16) == 7
     assert noise_report(params_for_bits(16))["digit_bits"] == 4
 
@@ -80,8 +81,8 @@ def test_fast_gadget_plan():
     from fheicp.params import _plan_worst, plan_cost
     F, F2 = (15, 2, 2), (23, 1, 2)
     want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F, F2, (4, 0, 1)), 12: (F, F2, (4, 0, 1)),
-            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 1, 3)), 17: (F, F2, (4, 1, 5)), 18: (F, F2, (4, 1, 5)),
-            19: (F, F2, (4, 1, 5))}
+            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 0, 3)), 17: (F, F2, (4, 1, 5)), 18: (F, F2, (4, 1, 5)),
+            19: (F, F2, (4, 1, 5)), 20: (F, F2, (4, 2, 5))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
         assert p.pbs_mid_level == 0, P
@@ -95,23 +96,24 @@ def test_fast_gadget_plan():
         assert fg2 is None or j2 == j1 or _plan_worst(p, d, j1, j2 - 1) < 9.2
         assert R == sign_pbs_count(p)
         assert plan_cost(p) < plan_cost(params_for_bits(P, fast=False))
-    # the headline width keeps its 4-bit digits: one bootstrap on the classic
-    # (15,2) gadget, two on its multi-bit form, four on multi-bit (23,1)
-    assert sign_plan(params_for_bits(16)) == (4, 1, 3)
+    # the headline width keeps its 4-bit digits, with no bootstrap on the
+    # classic (15,2) gadget since the (3, 5) key switch: three on its
+    # multi-bit form, four on multi-bit (23,1)
+    assert sign_plan(params_for_bits(16)) == (4, 0, 3)
     assert sign_plan(params_for_bits(19, fast=False)) == (4, 9, 9)
     assert params_for_bits(3).pbs_fast_level == 0
 
 
 def test_mid_gadget_plan():
-    """Mid gadgets: at P = 20 and from P = 22 the plan adds one or two
+    """Mid gadgets: from P = 21 the plan adds one or two
     cheaper main gadgets between the main and the fast one. The schedule walks
     main -> mid -> mid2 -> fast -> fast2, each gadget on the fewest rounds for
     which the next one on all the rest keeps every decision at 9.2 sigma, and
     the plan is cheaper than the same gadgets without mids."""
     from dataclasses import replace
     from fheicp.params import _sched_worst, plan_cost, sign_schedule
-    want = {20: ((15, 2), None), 21: ((12, 3), None), 22: ((12, 3), None), 23: ((12, 3), None),
-            24: ((8, 5), (12, 3)), 25: ((10, 4), (12, 3)), 26: ((8, 5), (12, 3)), 27: ((8, 5), (12, 3))}
+    want = {21: ((12, 3), None), 22: ((12, 3), None), 23: ((12, 3), None),
+            24: ((10, 4), (12, 3)), 25: ((10, 4), (12, 3)), 26: ((8, 5), (12, 3)), 27: ((8, 5), (12, 3))}
     for P, (m1, m2) in want.items():
         p = params_for_bits(P)
         assert (p.pbs_mid_base_log, p.pbs_mid_level) == m1, P
@@ -128,8 +130,14 @@ def test_mid_gadget_plan():
                 assert _sched_worst(p, d, fewer) < 9.2, (P, i)
         nomid = replace(p, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid2_base_log=0, pbs_mid2_level=0)
         assert plan_cost(p) < plan_cost(nomid), P
-    # C5's width: 1 main (6,7), 2 mid (8,5), 3 mid2 (12,3), 5 fast, 6 fast2
-    assert sign_schedule(params_for_bits(26))[1] == [0, 3, 3, 4, 4, 4] + [1] * 5 + [2] * 6
+    # C5's width: 1 main (5,8), 2 mid (8,5), 2 mid2 (12,3), 4 fast, 4 fast2
+    p26 = params_for_bits(26)
+    assert (p26.pbs_base_log, p26.pbs_level, p26.pbs_mid_base_log, p26.pbs_mid_level,
+            p26.pbs_mid2_base_log, p26.pbs_mid2_level) == (5, 8, 8, 5, 12, 3)
+    assert sign_schedule(p26)[1] == [0, 3, 3, 4, 4] + [1] * 4 + [2] * 4
+    # the headline width runs every round on the multi-bit fast gadgets: the
+    # main (15, 2) key is made but never launched
+    assert sign_schedule(params_for_bits(16))[1] == [1, 1, 1, 2, 2, 2, 2]
     # the headline width has no mid gadget; C3's (P = 21) takes the more
     # precise (10,4) main gadget, whose quieter first bootstrap allows 4-bit
     # digits: 10 bootstraps instead of 13
@@ -150,7 +158,7 @@ def test_multibit_noise_model():
         v1, v2 = _variances(p)[0], _variances(p, group=2)[0]
         assert 1.05 < v2 / v1 < 1.8, (b, lv, v2 / v1)
     # a plan whose fast gadget flips to classic when the group changes differs
-    q = params_for_bits(16)
+    q = params_for_bits(17)
     assert q.pbs_fast_group == 2 and q.pbs_fast2_group == 2
     assert sign_plan(replace(q, pbs_fast_group=1, pbs_fast2_group=1)) != sign_plan(q)
 
