@@ -63,9 +63,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-compares", type=int, default=0,
                     help="oracle sample size (0: 32 compares scaled down by the sign plan's cost, 10-30 s)")
-    ap.add_argument("--mode", choices=("compare", "corpus"), default="compare",
+    ap.add_argument("--mode", choices=("compare", "corpus", "embed"), default="compare",
                     help="compare: the reference's path (configs[1]); corpus: search over a stored corpus of "
-                         "seeded-LWE documents (SURVEY.md §8f-1)")
+                         "seeded-LWE documents (SURVEY.md §8f-1); embed: the BERT encoder of the embedding "
+                         "stage (SURVEY.md §8f-4)")
+    ap.add_argument("--embed-batch", type=int, default=256, help="--mode embed: sequences per forward pass")
+    ap.add_argument("--seq-len", type=int, default=100, help="--mode embed: tokens per sequence (max_length)")
     return ap.parse_args()
 
 
@@ -264,6 +267,8 @@ def main():
     _lib.lib()  # loud failure if the HIP library is missing
     if args.mode == "corpus":
         return corpus_main(args, world, rank, local, dev)
+    if args.mode == "embed":
+        return embed_main(args, world, rank, local, dev)
 
     model = build_model(args)
     model.compile(key_seed=args.seed, device=local)
@@ -630,6 +635,99 @@ def corpus_cpu_leg(args, c, bodies, ids, oq, cq, q_np, docs_np, P, parity):
                       f"expand seeded docs + linear + decrypt + {R.sign_pbs_count(dict(p0, msg_bits=P))} KS+PBS "
                       f"sign extraction + decrypt",
             "seconds": round(t_total, 2)}
+
+
+BF16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def embed_main(args, world, rank, local, dev):
+    """--mode embed: the embedding stage's encoder (fheicp.bert.GpuBert, the
+    forward of bert_embeddings.py:102-158) on a randomly initialised
+    bert-base (the weights are an offline download; synthetic token ids,
+    every sequence --seq-len tokens). One step = one forward pass + mean
+    pooling of --embed-batch sequences. Roofline: the bf16 MFMA GEMMs
+    (algorithmic 2*M*N*K per launch over their HIP-event time) against the
+    dense bf16 peak; the CPU baseline is the reference's own torch fp32
+    forward on the host cores, on a bounded sample."""
+    from transformers import BertConfig, BertModel
+    from fheicp.bert import GpuBert
+    torch.manual_seed(args.seed)
+    m = BertModel(BertConfig(), add_pooling_layer=False).eval()
+    g = GpuBert(model=m, device=local)
+    B, S = args.embed_batch, args.seq_len
+    gen = torch.Generator().manual_seed(args.seed + rank)
+    ids = torch.randint(1000, 30000, (B, S), generator=gen)
+    ids[:, 0] = 101
+    ids[:, -1] = 102
+    mask = torch.ones_like(ids)
+    ids_d, mask_d = ids.to(dev, torch.int32), mask.to(dev, torch.int32)
+    for _ in range(args.warmup):
+        g.forward(ids_d, mask_d)
+    torch.cuda.synchronize()
+    g.profile(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = g.forward(ids_d, mask_d)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    g.profile(False)
+    prof = {k: g.profile_read(k) for k in ("gemm", "attention", "other")}
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    seqs = world * B * args.steps
+    gm = prof["gemm"]
+    tf = gm["flops"] / (gm["total_ms"] * 1e-3) / 1e12 if gm["total_ms"] else 0.0
+    # agreement with the fp32 torch forward on the first sequences (tolerance: tests/test_gpu_bert.py)
+    n_chk = min(4, B)
+    with torch.no_grad():
+        ref = m(input_ids=ids[:n_chk], attention_mask=mask[:n_chk]).last_hidden_state.mean(1).double()
+    got = out[:n_chk].cpu().double()
+    cos = float(torch.nn.functional.cosine_similarity(got, ref, dim=1).min())
+    out_line = {
+        "metric": "BERT embeddings/sec (encoder forward + mean pooling) [embedding stage, SURVEY.md §8f-4]",
+        "value": round(seqs / elapsed, 2), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init bert-base, random ids)",
+        "config": {"workload": f"bert-base forward, {B} sequences x {S} tokens per GPU, mean pooling",
+                   "batch": B, "seq_len": S, "tokens_per_step": B * S * world, "parallelism": f"replicas{world}"},
+        "tokens_per_sec": round(seqs * S / elapsed, 1),
+        "roofline": {"bound": "mfma", "kernel": "fbert::k_gemm<EPI>", "achieved": round(tf, 2),
+                     "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / BF16_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": None, "gemm_ms_per_step": round(gm["total_ms"] / args.steps, 3),
+                     "gemm_launches_per_step": gm["launches"] // max(args.steps, 1),
+                     "gemm_flops_per_step": gm["flops"] / max(args.steps, 1),
+                     "attention_ms_per_step": round(prof["attention"]["total_ms"] / args.steps, 3),
+                     "other_ms_per_step": round(prof["other"]["total_ms"] / args.steps, 3)},
+        "parity": {"sequences_checked": n_chk, "min_cosine_vs_fp32_torch": round(cos, 6),
+                   "tolerance": "cosine >= 0.9995 (tests/test_gpu_bert.py)", "within_tolerance": cos >= 0.9995},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = torch.get_num_threads()
+        nb = 8
+        with torch.no_grad():
+            m(input_ids=ids[:2], attention_mask=mask[:2])
+            t0 = time.perf_counter()
+            reps = 0
+            while time.perf_counter() - t0 < 10.0:
+                m(input_ids=ids[:nb], attention_mask=mask[:nb])
+                reps += 1
+            el = time.perf_counter() - t0
+        out_line["cpu_baseline"] = {"value": round(reps * nb / el, 3), "unit": "sequences/s", "cores": cores,
+                                    "kind": "reference",
+                                    "sample": f"{reps} x {nb} sequences of {S} tokens through the same model in torch "
+                                              f"fp32 on the host (the reference's BertEmbedder forward, "
+                                              f"bert_embeddings.py:136), {cores} threads"}
+    if rank == 0:
+        print(json.dumps(out_line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

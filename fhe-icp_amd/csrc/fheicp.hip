@@ -110,7 +110,7 @@ static int validate(const fhe_params* p, std::string& why) {
     why = "pbs decomposition out of range"; return -1;
   }
   if (p->ks_level < 1 || p->ks_level > 8 || p->ks_base_log < 1 || p->ks_base_log > 7 ||
-      p->ks_level * p->ks_base_log > 62) {
+      p->ks_level * p->ks_base_log + p->ks_level > 63) {
     why = "ks decomposition out of range (base_log <= 7 for int8 digits)"; return -1;
   }
   if (p->msg_bits < 2 || p->msg_bits > 40) { why = "msg_bits must be in [2, 40]"; return -1; }
@@ -375,7 +375,7 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   if (const char* e = getenv("FHEICP_KS_VARIANT")) ctx->ks_variant = atoi(e) == 1 ? 1 : 2;
   // the MFMA key switch: digits in i8, K = kN * ks_level level-major in
   // 64-blocks, |sum| <= K * 2^(beta-1) * 128 < 2^31 in the i32 accumulators
-  if ((params->k * params->N) % 64 != 0 || params->ks_level * params->ks_base_log > 32 ||
+  if ((params->k * params->N) % 64 != 0 || params->ks_level * params->ks_base_log > 31 ||
       params->ks_base_log > 8 ||
       (double)params->k * params->N * params->ks_level * std::ldexp(1.0, params->ks_base_log - 1) * 128 >= 2147483648.0)
     ctx->ks_variant = 1;

@@ -47,8 +47,20 @@ __global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, i
       const int q = e / KS_IC, ii = e % KS_IC;
       if (q < nct && i0 + ii < iend_all) {
         const u64 a = in[(size_t)(c0 + q) * (big + 1) + i0 + ii] << shift;
-        const u64 packed = decompose_packed(a, kbeta, KL);  // offset-binary already
-        for (int l = 1; l <= KL; ++l) dig[ii][l - 1][q] = (uint8_t)((packed >> ((KL - l) * kbeta)) & ((1u << kbeta) - 1));
+        // zero-mean digits in [-B/2, B/2] (as k_ks_digits), offset by B/2
+        const int prec = KL * kbeta;
+        u64 v = ((a >> (63 - prec)) + 1) >> 1;
+        const u64 B = 1ull << kbeta;
+        for (int l = KL; l >= 1; --l) {
+          const u64 low = v & (B - 1);
+          v >>= kbeta;
+          int64_t d = (int64_t)low;
+          if (low > half || (low == half && ((a >> (62 - prec - (KL - l))) & 1))) {
+            d -= (int64_t)B;
+            v += 1;
+          }
+          dig[ii][l - 1][q] = (uint8_t)(d + (int64_t)half);
+        }
       } else {
         for (int l = 0; l < KL; ++l) dig[ii][l][q] = (uint8_t)half;  // digit 0
       }
@@ -153,16 +165,24 @@ __global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, i
   const u64* src = in + (size_t)c * (big + 1);
   if (blockIdx.x == 0 && iq == 0) body[c] = (src[big] << shift) + add_body;
   const int prec = levels * beta;
+  const uint32_t half = 1u << (beta - 1);
   uint32_t packed[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) packed[s] = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    uint32_t r = (uint32_t)((((src[i0 + q] << shift) >> (63 - prec)) + 1) >> 1);
+    const u64 x = src[i0 + q] << shift;
+    uint32_t r = (uint32_t)(((x >> (63 - prec)) + 1) >> 1);
+    // coins for the ties: the bits of x just below the rounding bit
+    const uint32_t coins = (uint32_t)(x >> (63 - prec - 8));
 #pragma unroll
     for (int s = 0; s < 8; ++s) {  // LSB-first: digit s is level levels - 1 - s
       if (s >= levels) break;
-      const int d = __builtin_amdgcn_sbfe((int)r, s * beta, beta);
+      // zero-mean digits in [-B/2, B/2] (oracle decompose_ks): a tie at B/2
+      // is -B/2 (with a carry) when bit 62 - prec - s of x is set
+      const uint32_t low = __builtin_amdgcn_ubfe(r, s * beta, beta);
+      const uint32_t coin = (coins >> (7 - s)) & 1u;
+      const int d = (low > half || (low == half && coin)) ? (int)low - (1 << beta) : (int)low;
       r -= (uint32_t)d << (s * beta);
       packed[s] |= (uint32_t)(uint8_t)(int8_t)d << (8 * q);
     }

@@ -453,6 +453,33 @@ static void decompose(uint64_t x, int bl, int L, int64_t* d) {
   }
 }
 void ref_decompose(uint64_t x, int bl, int L, int64_t* d) { decompose(x, bl, L, d); }
+/* The key switch's digits: the same closest multiple, as L
+ * digits in [-B/2, B/2], a tie at B/2 taking the sign of a coin: the digit
+ * of LSB-first index j (level L - j) is -B/2 (with a carry) when bit
+ * 62 - prec - j of x is 1. Those bits lie below the rounding bit, so for
+ * uniform x they are fair and independent of the rounded value: every
+ * digit is then zero-mean with E[d^2] = (B^2 + 2) / 12, the noise model's
+ * factor, where digits in [-B/2, B/2) have mean -1/2 and put a
+ * key-dependent bias 0.5 * sum(KSK noise) on every key switch. (Needs
+ * prec + L <= 63, and the bits are fair only above any shift of the
+ * input: prec + L - 1 < 62 - shift; fhe_ctx_create checks the first.) */
+static void decompose_ks(uint64_t x, int bl, int L, int64_t* d) {
+  const int prec = L * bl;
+  uint64_t v = ((x >> (63 - prec)) + 1) >> 1;
+  const uint64_t B = (uint64_t)1 << bl, half = B >> 1;
+  for (int l = L; l >= 1; --l) {
+    const uint64_t low = v & (B - 1);
+    v >>= bl;
+    const uint64_t coin = (x >> (62 - prec - (L - l))) & 1;
+    if (low > half || (low == half && coin)) {
+      d[l - 1] = (int64_t)low - (int64_t)B;
+      v += 1;
+    } else {
+      d[l - 1] = (int64_t)low;
+    }
+  }
+}
+void ref_decompose_ks(uint64_t x, int bl, int L, int64_t* d) { decompose_ks(x, bl, L, d); }
 
 static void keyswitch1(const ref_params* P, const uint64_t* ksk, const uint64_t* in, uint64_t* out) {
   const int n = P->n, dimb = P->k * P->N, KL = P->ks_level;
@@ -460,7 +487,7 @@ static void keyswitch1(const ref_params* P, const uint64_t* ksk, const uint64_t*
   for (int t = 0; t < n; ++t) out[t] = 0;
   out[n] = in[dimb];
   for (int i = 0; i < dimb; ++i) {
-    decompose(in[i], P->ks_base_log, KL, d);
+    decompose_ks(in[i], P->ks_base_log, KL, d);
     for (int l = 0; l < KL; ++l) {
       if (!d[l]) continue;
       const uint64_t* row = ksk + ((size_t)i * KL + l) * (n + 1);

@@ -76,6 +76,7 @@ def lib():
         L.ref_sign_digit_bits.argtypes = [P]; L.ref_sign_digit_bits.restype = C.c_int
         L.ref_negacyclic_mul.argtypes = [u64p, u64p, u64p, C.c_int]
         L.ref_decompose.argtypes = [C.c_uint64, C.c_int, C.c_int, i64p]
+        L.ref_decompose_ks.argtypes = [C.c_uint64, C.c_int, C.c_int, i64p]
         L.ref_tuniform.argtypes = [C.c_uint64, C.c_int]; L.ref_tuniform.restype = C.c_int64
         L.ref_chacha20_block.argtypes = [u32p, C.c_uint32, u32p, u32p]
         L.ref_encrypt_seeded.argtypes = [P, u64p, i64p, C.c_int64, C.c_int32, u32p, u32p, u64p, u64p]
@@ -280,6 +281,13 @@ def negacyclic_mul(a, b) -> np.ndarray:
 def decompose(x: int, base_log: int, levels: int) -> np.ndarray:
     d = np.zeros(levels, np.int64)
     lib().ref_decompose(C.c_uint64(x), base_log, levels, i64(d))
+    return d
+
+
+def decompose_ks(x: int, base_log: int, levels: int) -> np.ndarray:
+    """The key switch's zero-mean digits (tfhe_ref.c decompose_ks)."""
+    d = np.zeros(levels, np.int64)
+    lib().ref_decompose_ks(C.c_uint64(x), base_log, levels, i64(d))
     return d
 
 

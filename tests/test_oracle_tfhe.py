@@ -310,3 +310,27 @@ def test_oracle_threshold_restatement(oracle_lib):
     acc = np.array([-(2 ** (P - 2)), T - 2, T - 1, T, T + 1, 2 ** (P - 2)], dtype=np.int64)
     bit = ref.threshold(ref.encrypt_ints(acc, seed=3), T)
     assert np.array_equal(ref.decrypt_bits(bit), (acc >= T).astype(np.int64))
+
+
+@pytest.mark.parametrize("beta,lvl", [(3, 5), (4, 4), (2, 8), (7, 4)])
+def test_keyswitch_digits_zero_mean(oracle_lib, beta, lvl):
+    """The key switch's digits (tfhe_ref.c decompose_ks, the same rule in
+    k_ks_digits and k_keyswitch): they recompose the input rounded to
+    lvl * beta bits modulo 2^64, lie in [-B/2, B/2], and are zero-mean with
+    E[d^2] = (B^2 + 2) / 12, the noise model's factor (fheicp.params): the
+    [-B/2, B/2) digits' mean of -1/2 would put a key-dependent bias
+    0.5 * sum(KSK noise) on every key switch (measured 7% above the model's
+    sigma on one (3, 5) key before this rule)."""
+    from oracle.tfhe_ref import decompose_ks
+    rng = np.random.default_rng(beta * 10 + lvl)
+    xs = [int(x) for x in rng.integers(0, 2 ** 63, 20000, dtype=np.uint64) * 2 + rng.integers(0, 2, 20000)]
+    prec = beta * lvl
+    B = 1 << beta
+    ds = np.array([decompose_ks(x, beta, lvl) for x in xs])
+    assert ds.min() >= -B // 2 and ds.max() <= B // 2
+    for x, d in zip(xs[:2000], ds[:2000]):
+        want = (((x >> (63 - prec)) + 1) >> 1) << (64 - prec)
+        got = sum(int(d[l]) << (64 - (l + 1) * beta) for l in range(lvl))
+        assert got % 2 ** 64 == want % 2 ** 64
+    assert abs(ds.mean()) < 0.02
+    assert abs((ds.astype(float) ** 2).mean() / ((B * B + 2) / 12) - 1) < 0.02
