@@ -144,13 +144,20 @@ def lib_sha256() -> str:
 
 
 def load_pmc() -> dict:
-    """Per-kernel PMC figures of THIS build ({} if the file was measured on
-    another libfheicp.so)."""
+    """Per-kernel PMC figures of THIS build, keyed "kernel@cts" ({} if the
+    file was measured on another libfheicp.so)."""
     try:
         d = json.loads(PMC_FILE.read_text())
     except (OSError, ValueError):
         return {}
     return d.get("kernels", {}) if d.get("lib_sha256") == lib_sha256() else {}
+
+
+def pmc_entry(pmc: dict, kernel: str, cts: int):
+    """(entry at this batch size or None, any entry of this kernel or None)."""
+    exact = pmc.get(f"{kernel}@{cts}")
+    anyk = exact or next((v for k, v in pmc.items() if k.rsplit("@", 1)[0] == kernel), None)
+    return exact, anyk
 
 
 def read_br(eng) -> dict:
@@ -174,9 +181,14 @@ def _br_kernel(q, br, pmc, group: int = 1) -> dict:
     bsk_bytes = ggsws * (q.k + 1) * q.pbs_level * (q.k + 1) * (q.N // 2) * 16
     io_bytes = cts_per_launch * ((q.n + 1) * 8 + (q.k * q.N + 1) * 8 * 5)
     alg_bytes = bsk_bytes + io_bytes
-    m = pmc.get(br["kernel"], {})
-    measured = bool(m) and int(m.get("cts_per_launch", -1)) == int(cts_per_launch)
-    flops = float(m["f64_flops_per_launch"]) if measured else br_flops_per_ct(q, group) * cts_per_launch
+    m, anyk = pmc_entry(pmc, br["kernel"], int(round(cts_per_launch)))
+    m = m or {}
+    # executed f64 FLOPs: PMC of this build (per padded ciphertext, so any
+    # batch of the same kernel); the analytic radix-2 count only when this
+    # kernel was never measured on this build (it over-counts by 14-20%)
+    padded = (int(round(cts_per_launch)) + 3) // 4 * 4
+    measured = anyk is not None and "f64_flops_per_ct" in anyk
+    flops = float(anyk["f64_flops_per_ct"]) * padded if measured else br_flops_per_ct(q, group) * cts_per_launch
     secs = avg_ms * 1e-3
     return {
         "kernel": br["kernel"], "gadget": [q.pbs_base_log, q.pbs_level], "group": group,
@@ -186,8 +198,10 @@ def _br_kernel(q, br, pmc, group: int = 1) -> dict:
         "achieved_tflops_f64": flops / secs / 1e12 if br["launches"] else 0.0,
         "alg_bytes_per_launch": int(alg_bytes),
         "achieved_gbs": alg_bytes / secs / 1e9 if br["launches"] else 0.0,
-        "hbm_bytes_per_launch": float(m["hbm_bytes_per_launch"]) if measured and "hbm_bytes_per_launch" in m else None,
-        "pmc_avg_launch_ms": m.get("avg_launch_ms") if measured else None,
+        # HBM bytes do not scale with the batch (each XCD's L2 streams the key once): exact batch only
+        "hbm_bytes_per_launch": float(m["hbm_bytes_per_launch"]) if "hbm_bytes_per_launch" in m else None,
+        "pmc_avg_launch_ms": m.get("avg_launch_ms"),
+        "pmc_command": (anyk or {}).get("command"),
     }
 
 

@@ -13,7 +13,9 @@ Recipe (MI355X_MICROARCH.md, HBM/rocprofv3): SQ_INSTS_* count wave64
 instructions, so f64 FLOPs = 64 x (2 FMA + ADD + MUL); FETCH_SIZE/WRITE_SIZE
 are KiB from separate passes and gfx950's FETCH_SIZE counts half the bytes of
 wide coalesced reads: hbm_bytes = (2 FETCH_SIZE + WRITE_SIZE) x 1024.
-Usage: br_pmc.py --lib LIB --cts N --f64 CSV --fetch CSV --write CSV [--trace CSV] --out JSON
+Entries are keyed "kernel@cts" (several configs merge into one file with
+--merge); f64_flops_per_ct scales to any batch of the same kernel.
+Usage: br_pmc.py --lib LIB --cts N --f64 CSV --fetch CSV --write CSV [--trace CSV] [--merge JSON] --out JSON
 """
 import argparse
 import collections
@@ -56,23 +58,37 @@ def main():
     ap.add_argument("--trace", default="")
     ap.add_argument("--command", default="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--merge", default="", help="an earlier br_pmc.json of the same library to extend")
     a = ap.parse_args()
     f64, fetch, write = per_kernel(a.f64), per_kernel(a.fetch), per_kernel(a.write)
     tr = trace_ms(a.trace) if a.trace else {}
-    out = {"lib_sha256": hashlib.sha256(open(a.lib, "rb").read()).hexdigest(), "command": a.command,
-           "cts_per_launch": a.cts, "kernels": {}}
+    sha = hashlib.sha256(open(a.lib, "rb").read()).hexdigest()
+    out = {"lib_sha256": sha, "commands": [], "kernels": {}}
+    if a.merge:
+        try:
+            old = json.load(open(a.merge))
+            if old.get("lib_sha256") == sha:
+                out["commands"] = old.get("commands", [])
+                out["kernels"] = old.get("kernels", {})
+        except (OSError, ValueError):
+            pass
+    out["commands"].append({"command": a.command, "cts_per_launch": a.cts})
+    # the blind-rotation kernels run whole workgroups of 4 ciphertexts, so
+    # their work per launch is (f64 FLOPs per padded ciphertext) x ceil(cts/4)*4
+    padded = (a.cts + 3) // 4 * 4
     for n, c in f64.items():
         fma, add, mul = (c.get(f"SQ_INSTS_VALU_{x}_F64", (0.0, 0))[0] for x in ("FMA", "ADD", "MUL"))
+        flops = 64.0 * (2 * fma + add + mul)
         e = {"cts_per_launch": a.cts, "launches": c.get("SQ_INSTS_VALU_FMA_F64", (0, 0))[1],
              "f64_insts_per_launch": {"fma": fma, "add": add, "mul": mul},
              "valu_insts_per_launch": c.get("SQ_INSTS_VALU", (0.0, 0))[0],
-             "f64_flops_per_launch": 64.0 * (2 * fma + add + mul)}
+             "f64_flops_per_launch": flops, "f64_flops_per_ct": flops / padded, "command": a.command}
         if n in fetch and n in write:
             fk, wk = fetch[n]["FETCH_SIZE"][0], write[n]["WRITE_SIZE"][0]
             e.update(fetch_size_kib=fk, write_size_kib=wk, hbm_bytes_per_launch=(2 * fk + wk) * 1024)
         if n in tr:
             e["avg_launch_ms"], e["trace_launches"] = tr[n]
-        out["kernels"][n] = e
+        out["kernels"][f"{n}@{a.cts}"] = e
     s = json.dumps(out, indent=1)
     open(a.out, "w").write(s + "\n")
     print(s)

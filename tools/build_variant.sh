@@ -6,4 +6,4 @@ set -e
 HERE=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result "$@" \
-  -o "$HERE/fhe-icp_amd/fheicp/libfheicp_$name.so" "$HERE/fhe-icp_amd/csrc/fheicp.hip"
+  -o "$HERE/fhe-icp_amd/fheicp/libfheicp_$name.so" "$HERE/fhe-icp_amd/csrc/fheicp.hip" "$HERE/fhe-icp_amd/csrc/bert.hip"

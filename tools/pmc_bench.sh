@@ -3,7 +3,9 @@
 # own run, as the gfx950 recipe requires) and the per-kernel summary bench.py
 # reads: gpurun_out/pmc_bench/br_pmc.json (copy it to profiles/br_pmc.json).
 # Extra bench.py arguments (another config) go in $BENCH_ARGS; $CTS is the
-# ciphertexts per launch (the documents per GPU of that run).
+# ciphertexts per launch (the documents per GPU of that run); a run for another
+# config merges into the same file (entries keyed kernel@cts); $PMC_ENV names
+# an environment prefix of the command in the record (e.g. "FHEICP_PIPE=0 ").
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/pmc_bench; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
 CMD="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}"
@@ -16,4 +18,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
 python3 tools/br_pmc.py --lib fhe-icp_amd/fheicp/libfheicp.so --cts "${CTS:-1024}" --f64 "$(csvof "$OUT/f64")" \
   --fetch "$(csvof "$OUT/fetch")" --write "$(csvof "$OUT/write")" \
   --trace "$(ls "$OUT"/trace/*kernel_trace.csv "$OUT"/trace/*/*kernel_trace.csv 2>/dev/null | head -n1)" \
-  --command "python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}" --out "$OUT/br_pmc.json" > "$OUT/br_pmc.log" 2>&1
+  --command "${PMC_ENV:-}python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}" \
+  --merge "${PMC_MERGE:-$OUT/br_pmc.json}" --out "$OUT/br_pmc.json" > "$OUT/br_pmc.log" 2>&1
