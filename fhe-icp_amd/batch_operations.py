@@ -51,6 +51,9 @@ from fhe_similarity import FHESimilarityModel
 logger = logging.getLogger(__name__)
 
 FHE_MODES = ("execute", "simulate", "disable")
+# which reducer produced a stored vector (BatchConfig.gpu_reducer)
+REDUCER_KEY = "fheicp_reducer"
+GPU_REDUCER = "gpu-pca-f64"
 
 
 @dataclass
@@ -68,7 +71,17 @@ class BatchConfig:
     input_dim: int = field(default_factory=lambda: int(os.environ.get("FHE_ICP_DIM", "128")))
     n_bits: int = field(default_factory=lambda: int(os.environ.get("FHE_ICP_N_BITS", "8")))
     reducer_path: str = "pca_reducer_128.pkl"  # DimensionReducer.load (:63)
-    gpu_reducer: bool = False       # run a fitted PCA DimensionReducer on the GPU (fheicp.pca, §8f-4)
+    # run a fitted PCA DimensionReducer on the GPU (fheicp.pca, §8f-4).
+    # Tolerance: the GPU transform accumulates in f64 and rounds once to
+    # float32; sklearn's float32 BLAS sums in an unspecified order. The two
+    # agree to ~1e-5 relative, so a feature can land on the other side of an
+    # input-quantizer rounding boundary (one quantization level, hence a
+    # different accumulator) than in a CPU-reduced store. Documents written
+    # with gpu_reducer carry metadata[REDUCER_KEY] = GPU_REDUCER; searches and
+    # compares refuse to mix the two reducers (ValueError) unless
+    # allow_mixed_reducers, and are bit-exact within one reducer's vectors.
+    gpu_reducer: bool = False
+    allow_mixed_reducers: bool = False
     key_manager_default: bool = True  # no key_manager given: FHEKeyManager() as the reference (:64)
     device: int = 0
     model_path: Optional[str] = None  # fheicp.persist file: load instead of retrain (§8f-2)
@@ -285,6 +298,8 @@ class BatchProcessor:
                           metadata: Optional[List[Dict]] = None) -> List[str]:
         """Embed, reduce and store documents (:120-204): one index rewrite per batch."""
         self._require_model()
+        self._check_reducers(list(self.storage.index.keys()), GPU_REDUCER if self.config.gpu_reducer else None,
+                             query=True)
         n = len(texts)
         if doc_ids is None:
             stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
@@ -297,7 +312,10 @@ class BatchProcessor:
             if self._check_memory() > self.config.max_memory_mb:
                 self._maybe_gc()
             vecs = self._embed(texts[s:e])
-            docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs, key_id, metadata[s:e])
+            meta = metadata[s:e]
+            if self.config.gpu_reducer:
+                meta = [dict(m, **{REDUCER_KEY: GPU_REDUCER}) for m in meta]
+            docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs, key_id, meta)
             self.storage.save_many(docs)
             out.extend(d.doc_id for d in docs)
             if (s + self.config.batch_size) % self.config.checkpoint_interval == 0:
@@ -336,8 +354,25 @@ class BatchProcessor:
             out.extend(d.doc_id for d in docs)
         return out
 
+    def _reducer_of(self, doc_id: str):
+        return self.storage.index[doc_id].get("metadata", {}).get(REDUCER_KEY)
+
+    def _check_reducers(self, doc_ids, query_reducer=None, query: bool = False):
+        """The GPU-PCA contract (BatchConfig.gpu_reducer): the vectors that
+        meet in one score come from one reducer."""
+        if self.config.allow_mixed_reducers:
+            return
+        seen = {self._reducer_of(i) for i in doc_ids if i in self.storage.index}
+        if query:
+            seen.add(query_reducer)
+        if len(seen) > 1:
+            raise ValueError(f"vectors from different dimension reducers {sorted(map(str, seen))} would meet in one "
+                             "score: the GPU and CPU PCA differ at quantizer rounding boundaries "
+                             "(BatchConfig.gpu_reducer, allow_mixed_reducers)")
+
     def compare_encrypted(self, doc_id1: str, doc_id2: str) -> float:
         self._require_model()
+        self._check_reducers([doc_id1, doc_id2])
         d1, d2 = self.storage.load(doc_id1), self.storage.load(doc_id2)
         if self.storage.holds_ciphertexts() or d1.model_version != "1.0" or d2.model_version != "1.0":
             return self._compare_ciphertexts(d1, d2)
@@ -368,6 +403,8 @@ class BatchProcessor:
     def search_similar(self, query_text: str, top_k: int = 5, min_similarity: float = 0.5) -> List[Tuple[str, float]]:
         self._require_model()
         embedder, reducer = self._upstream()
+        self._check_reducers(list(self.storage.index.keys()),
+                             GPU_REDUCER if self.config.gpu_reducer else None, query=True)
         q = embedder.get_embedding(query_text)
         q = reducer.transform(np.asarray(q).reshape(1, -1))[0]
         return self.search_vector(q, top_k, min_similarity)

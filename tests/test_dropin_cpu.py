@@ -376,3 +376,44 @@ def test_corpus_secret_checked_before_keygen(tmp_path, monkeypatch):
     monkeypatch.delenv("FHE_MASTER_PASSWORD", raising=False)
     with pytest.raises(ValueError, match="password"):
         _processor(tmp_path, fhe="execute", store_ciphertexts=True, corpus_path=str(tmp_path / "c.npz"))
+
+
+class _GpuTaggedReducer(_Reducer):
+    """A reducer the processor takes as already on the device (it has
+    transform_dev), standing in for fheicp.pca.GpuPCA on a host without one."""
+
+    def transform_dev(self, X):  # pragma: no cover - never called here
+        raise AssertionError
+
+
+def test_gpu_reducer_contract_refuses_mixed_stores(tmp_path):
+    """BatchConfig.gpu_reducer: documents reduced on the GPU are tagged, and a
+    score never mixes GPU- and CPU-reduced vectors (the two PCAs differ at
+    quantizer rounding boundaries): searching, comparing or adding across
+    reducers raises unless allow_mixed_reducers."""
+    from batch_operations import GPU_REDUCER, REDUCER_KEY, BatchConfig, BatchProcessor
+    from encrypted_storage import EncryptedDocumentStore
+    store = EncryptedDocumentStore(str(tmp_path))
+
+    def proc(**kw):
+        c = BatchConfig(**{"fhe": "disable", "input_dim": 16, "n_bits": 6, "seed": 21, "show_progress": False,
+                           "key_manager_default": False, **kw})
+        red = _GpuTaggedReducer() if kw.get("gpu_reducer") else _Reducer()
+        return BatchProcessor(embedder=_Embedder(), reducer=red, storage=store, config=c)
+
+    g = proc(gpu_reducer=True)
+    g.encrypt_documents(["alpha doc", "beta doc", "gamma doc"], doc_ids=["a", "b", "c"])
+    assert all(store.index[i]["metadata"][REDUCER_KEY] == GPU_REDUCER for i in "abc")
+    assert len(g.search_similar("alpha doc", top_k=2, min_similarity=-100)) == 2   # one reducer: fine
+    cpu = proc()
+    with pytest.raises(ValueError, match="reducers"):
+        cpu.search_similar("alpha doc", top_k=2, min_similarity=-100)
+    with pytest.raises(ValueError, match="reducers"):
+        cpu.encrypt_documents(["delta doc"], doc_ids=["d"])
+    mixed = proc(allow_mixed_reducers=True)
+    mixed.encrypt_documents(["delta doc"], doc_ids=["d"])
+    assert REDUCER_KEY not in store.index["d"]["metadata"]
+    with pytest.raises(ValueError, match="reducers"):
+        g.compare_encrypted("a", "d")
+    assert isinstance(mixed.compare_encrypted("a", "d"), float)
+    assert g.compare_encrypted("a", "b") == pytest.approx(mixed.compare_encrypted("a", "b"))

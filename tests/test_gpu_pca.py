@@ -65,3 +65,63 @@ def test_pca_then_encrypted_compare(need_gpu):
     oq = Q.QuantizedLinearParams.from_json(m.qparams.to_dict())
     assert np.array_equal(acc.cpu().numpy(), Q.accumulate(oq, Q.quantize_input(oq, Q.pair_features(q, docs))))
     g.close()
+
+
+def test_reducer_contract_at_quantizer_boundaries(need_gpu, tmp_path):
+    """The contract of BatchConfig.gpu_reducer, at a quantizer rounding
+    boundary (dimension_reduction.py:67-72 feeding batch_operations.py:226,
+    :273): the GPU PCA and sklearn's float32 PCA differ in the last float32
+    bits, and a query that puts a rounding boundary of the input quantizer
+    between the two values of a feature makes the quantized inputs (hence the
+    accumulator) differ. So a store reduced by one is never scored against
+    vectors from the other: the processor refuses the mix, and within the GPU
+    reducer every score equals the oracle on the GPU-reduced vectors."""
+    from sklearn.decomposition import PCA
+    from oracle import quant_ref as Q
+    from batch_operations import GPU_REDUCER, REDUCER_KEY, BatchConfig, BatchProcessor
+    from encrypted_storage import EncryptedDocument, EncryptedDocumentStore
+    from fheicp.pca import GpuPCA
+    rng = np.random.default_rng(9)
+    train = rng.standard_normal((1500, 768)).astype(np.float32)
+    pca = PCA(n_components=16, random_state=42).fit(train)
+    g = GpuPCA.from_sklearn(pca, 0)
+    X = rng.standard_normal((400, 768)).astype(np.float32)
+    got, ref32 = g.transform(X), pca.transform(X).astype(np.float32)
+    diff = np.argwhere(got != ref32)
+    assert len(diff) > 0                                  # the reducers differ in the last bits
+    i, j = map(int, diff[0])
+    a, b = sorted((float(ref32[i, j]), float(got[i, j])))
+    Xt, yt = Q.prepare_training_data(16, 1000, seed=11)
+    qp = Q.fit_quantized_linear(Xt, yt, 6)
+    # a query component that puts the quantizer boundary (k + 1/2 - zp) s between q_j a and q_j b
+    k = int(np.floor(0.5 * (qp.qx_max + qp.qx_min))) + 3
+    boundary = (k + 0.5 - qp.zp_x) * qp.s_x
+    qj = boundary / (0.5 * (a + b))
+    query = np.zeros(16, np.float64)
+    query[j] = qj
+    fa = Q.quantize_input(qp, Q.pair_features(query, ref32[i][None, :]))
+    fb = Q.quantize_input(qp, Q.pair_features(query, got[i][None, :]))
+    assert fa[0, j] != fb[0, j]                           # one quantization level apart
+    # the processor: GPU-reduced documents are tagged, a CPU-reduced query is refused
+    class Emb:
+        def get_embedding(self, t):
+            return X[int(t.split()[1])]
+
+        def get_embeddings_batch(self, ts):
+            return np.stack([self.get_embedding(t) for t in ts])
+    store = EncryptedDocumentStore(str(tmp_path))
+    cfg = BatchConfig(fhe="execute", input_dim=16, n_bits=6, seed=11, key_seed=12, gpu_reducer=True,
+                      show_progress=False, key_manager_default=False)
+    p = BatchProcessor(embedder=Emb(), reducer=g, storage=store, config=cfg)
+    texts = [f"doc {r}" for r in range(64)]
+    p.encrypt_documents(texts, doc_ids=[f"d{r}" for r in range(64)])
+    assert all(store.index[f"d{r}"]["metadata"][REDUCER_KEY] == GPU_REDUCER for r in range(64))
+    res = p.search_similar("doc 70", top_k=5, min_similarity=-100.0)
+    oq = Q.QuantizedLinearParams.from_json(p.fhe_model.model.quant_params.to_dict())
+    assert res == Q.search(oq, got[70], got[:64], 5, -100.0, doc_ids=[f"d{r}" for r in range(64)])
+    cpu = BatchProcessor(embedder=Emb(), reducer=pca, storage=store,
+                         config=BatchConfig(fhe="disable", input_dim=16, n_bits=6, seed=11, show_progress=False,
+                                            key_manager_default=False))
+    with pytest.raises(ValueError, match="reducers"):
+        cpu.search_similar("doc 70", top_k=5, min_similarity=-100.0)
+    g.close()
