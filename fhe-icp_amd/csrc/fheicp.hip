@@ -144,8 +144,9 @@ static int validate(const fhe_params* p, std::string& why) {
     const int L = g == 1 ? p->pbs_fast_level : p->pbs_fast2_level;
     const int bl = g == 1 ? p->pbs_fast_base_log : p->pbs_fast2_base_log;
     if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group must be 0, 1 or 2"; return -1; }
-    if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 2 && L * bl <= 31)) {
-      why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 2, level * base_log <= 31";
+    (void)bl;  // 32-bit accumulators when level <= 2 and level * base_log <= 31, else 64-bit (k_blind_rotate_mb64)
+    if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 8)) {
+      why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 8";
       return -1;
     }
   }
@@ -1032,6 +1033,25 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       name = "k_blind_rotate_mb<DBG>";
     } else
 #endif
+    // 64-bit accumulators (L * beta > 31 or L > 2): the deep gadgets
+    if (!(p.pbs_level <= 2 && p.pbs_level * p.pbs_base_log <= 31)) {
+#define MB64(L)                                                                                                  \
+  hipLaunchKernelGGL((k_blind_rotate_mb64<L, 0>), gm, bm, 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft,   \
+                     ctx->tw4, ctx->psi, tv, mode, out, ct_v, refreshed, sign);                                 \
+  name = "k_blind_rotate_mb64<" #L ", 0>"
+      switch (p.pbs_level) {
+        case 1: MB64(1); break;
+        case 2: MB64(2); break;
+        case 3: MB64(3); break;
+        case 4: MB64(4); break;
+        case 5: MB64(5); break;
+        case 6: MB64(6); break;
+        case 7: MB64(7); break;
+        case 8: MB64(8); break;
+        default: return fail(ctx, FHE_E_ARG, "multi-bit blind rotation: pbs_level > 8");
+      }
+#undef MB64
+    } else
     // the shipped fast gadgets (23,1) and (15,2) with their base log fixed
     if (p.pbs_level == 1 && p.pbs_base_log == 23) {
       MBD(1, 0, 23);

@@ -708,16 +708,20 @@ __host__ __device__ constexpr int psi_pos(int x) { return x ^ ((x >> 4) & 15); }
 // which folds the digit shifts and widths into inline operands; 0 = `beta`.
 // Key rows come through buffer loads: a per-lane offset fixed for the kernel
 // and a scalar offset per row, so the loads take no VALU address arithmetic.
-template <int L, int DBG = 0, int BETA = 0>
-__global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u64* __restrict__ small, int64_t count, int n,
-                                                                      int beta, const c64* __restrict__ bsk,
-                                                                      const c64* __restrict__ tw4,
-                                                                      const c64* __restrict__ psi, BrTv tv, int mode,
-                                                                      u64* __restrict__ out, u64* __restrict__ ct_v,
-                                                                      u64* __restrict__ refreshed, u64* __restrict__ sign) {
+// A32: 32-bit accumulators (L * beta <= 31, k_blind_rotate_mb); else 64-bit
+// ones (k_blind_rotate_mb64, the deep gadgets): the accumulator words are u64
+// with v4s's two-word rounding, and from L = 3 the level loop stays rolled and
+// each level's digits are read from the accumulator plus the rounding and
+// balancing offset (decompose_v4's offset form) instead of being kept.
+template <int L, int DBG, int BETA, bool A32>
+__device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t count, int n, int beta,
+                                          const c64* __restrict__ bsk, const c64* __restrict__ tw4,
+                                          const c64* __restrict__ psi, BrTv tv, int mode, u64* __restrict__ out,
+                                          u64* __restrict__ ct_v, u64* __restrict__ refreshed, u64* __restrict__ sign) {
   using namespace v4;
-  using AT = Acc<true>;
-  using T = uint32_t;
+  using AT = Acc<A32>;
+  using T = typename AT::T;
+  constexpr bool ROLL = !A32 && L >= 3;
   constexpr int G = 4, NT = nthreads(G), NPSI = 2 * N;
   constexpr int OFF_TW = NPSI, OFF_X = OFF_TW + NTW, NC64 = OFF_X + G * WPC * SCR;
   __shared__ c64 lds[NC64];
@@ -746,7 +750,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
   // 4.02 -> 3.97 ms per 1024 (NR = 2 slower, 6 and 8 no better then). With the
   // wave priorities of BR_PRIO the kernel fell to 148 VGPRs, and all eight fit:
   // 3.77 -> 3.73 ms (NR = 6: 3.75; profiles/r02g_treg_ab.txt)
-  constexpr int NR = L == 1 ? FHEICP_MB_TREG : 0;
+  constexpr int NR = (L == 1 && A32) ? FHEICP_MB_TREG : 0;
   c64 treg[NR > 0 ? NR : 1];
 #pragma unroll
   for (int m = 0; m < NR; ++m) treg[m] = tw4[m * 64 + lane];
@@ -777,6 +781,19 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
   }
 
   constexpr int R = WPC * L;  // GGSW rows per subset
+  // 64-bit accumulators: digit lv of word x is the plain beta-bit field of
+  // x + coff minus B/2 (decompose_v4's offset form, the same digits)
+  const int prec = L * bta;
+  u64 coff = 0;
+  if constexpr (!A32) {
+    coff = (u64)1 << (63 - prec);
+    for (int l = 0; l < L; ++l) coff += (u64)1 << (64 - prec + l * bta + bta - 1);
+  }
+  auto digit_at = [&](T x, int lv) -> double {
+    const u64 rr = (u64)x + coff;
+    return (double)((int)((uint32_t)(rr >> (64 - prec + (L - 1 - lv) * bta)) & ((1u << bta) - 1u)) -
+                    (1 << (bta - 1)));
+  };
   for (int j = 0; j < np; ++j) {
     [[maybe_unused]] unsigned long long stamp_[16];
     V4_STAMP(0);
@@ -789,15 +806,19 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       aS[gg][2] = (aS[gg][0] + aS[gg][1]) & (2 * N - 1);
     }
     c64 v[S];
-    uint32_t dg[L > 1 ? L - 1 : 1][S];
+    uint32_t dg[(L > 1 && A32) ? L - 1 : 1][S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      int d[2][L];
+      if constexpr (A32) {
+        int d[2][L];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) decompose_v4<L, true>(acc[s + h * S], bta, d[h]);
-      v[s] = {(double)d[0][0], (double)d[1][0]};
+        for (int h = 0; h < 2; ++h) decompose_v4<L, true>(acc[s + h * S], bta, d[h]);
+        v[s] = {(double)d[0][0], (double)d[1][0]};
 #pragma unroll
-      for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
+        for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
+      } else {
+        v[s] = {digit_at(acc[s], 0), digit_at(acc[s + S], 0)};
+      }
     }
     V4_STAMP(1);
     if constexpr (br_prio_fine<L>()) MB_PRIO(1);
@@ -805,12 +826,17 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) o[gg][0] = o[gg][1] = {0.0, 0.0};
     const int kjoff = j * 3 * R * WPC * M * (int)sizeof(c64);  // this pair's key, bytes
-#pragma unroll
+    constexpr int UNROLL_LV = ROLL ? 1 : L;
+#pragma unroll UNROLL_LV
     for (int lv = 0; lv < L; ++lv) {
       if (lv > 0) {
 #pragma unroll
-        for (int u = 0; u < S; ++u)
-          v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+        for (int u = 0; u < S; ++u) {
+          if constexpr (A32)
+            v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
+          else
+            v[u] = {digit_at(acc[u], lv), digit_at(acc[u + S], lv)};
+        }
       }
       // key rows of this quarter, slot t: [subset][row] (9 per slot)
       c64 kb[2][3][WPC];
@@ -917,6 +943,27 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
       br_emit(mode, AT::to64(acc[0]), true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
     }
   }
+}
+
+template <int L, int DBG = 0, int BETA = 0>
+__global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u64* __restrict__ small, int64_t count, int n,
+                                                                      int beta, const c64* __restrict__ bsk,
+                                                                      const c64* __restrict__ tw4,
+                                                                      const c64* __restrict__ psi, BrTv tv, int mode,
+                                                                      u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                                      u64* __restrict__ refreshed, u64* __restrict__ sign) {
+  mb_rotate<L, DBG, BETA, true>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
+}
+// the deep gadgets (L * beta > 31) on the multi-bit rotation: 64-bit accumulators
+template <int L, int DBG = 0>
+__global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb64(const u64* __restrict__ small, int64_t count,
+                                                                        int n, int beta, const c64* __restrict__ bsk,
+                                                                        const c64* __restrict__ tw4,
+                                                                        const c64* __restrict__ psi, BrTv tv, int mode,
+                                                                        u64* __restrict__ out, u64* __restrict__ ct_v,
+                                                                        u64* __restrict__ refreshed,
+                                                                        u64* __restrict__ sign) {
+  mb_rotate<L, DBG, 0, false>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
 }
 
 // ---- classic blind rotation with key-stationary products ---------------------

@@ -44,6 +44,10 @@ INSTANCES = {
     # the multi-bit kernels with a run-time base log (other gadgets)
     (14, 2, 2): "k_blind_rotate_mb<2, 0, 0>",
     (22, 1, 2): "k_blind_rotate_mb<1, 0, 0>",
+    # the deep gadgets on the multi-bit rotation, 64-bit accumulators
+    (12, 3, 2): "k_blind_rotate_mb64<3, 0>",
+    (10, 4, 2): "k_blind_rotate_mb64<4, 0>",
+    (8, 5, 2): "k_blind_rotate_mb64<5, 0>",
 }
 COUNT = 4096
 TV = 1 << 61
@@ -74,7 +78,9 @@ def test_bootstrap_noise_vs_model(need_gpu, oracle_lib, gadget):
     out = eng.pbs_gadget(small, g, TV)
     eng.profile(False)
     assert eng.kernel_name(bucket) == INSTANCES[gadget]
-    assert eng.profile_read(bucket)["items"] == COUNT
+    prof = eng.profile_read(bucket)
+    assert prof["items"] == COUNT
+    print(f"gadget {gadget}: {prof['total_ms'] / prof['launches'] * 1024 / COUNT:.3f} ms per 1024 bootstraps")
     ph = signed(u64(eng.phase(out)))
     err = (ph - sgn * TV).astype(np.float64) / 2.0 ** 64
     sigma = float(np.sqrt(np.mean(err ** 2)))   # RMS: a bias would count too
