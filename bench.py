@@ -227,16 +227,12 @@ def roofline(p, brs, batch: int = 0) -> dict:
     five gadgets run; the kernel with the largest total time is reported, all
     are listed under `kernels`."""
     from dataclasses import replace
-    qs = {"main": (p, 1)}
-    for g, bl, lv in (("mid", p.pbs_mid_base_log, p.pbs_mid_level), ("mid2", p.pbs_mid2_base_log, p.pbs_mid2_level)):
-        if lv:
-            qs[g] = (replace(p, pbs_base_log=bl, pbs_level=lv), 1)
-    if p.pbs_fast_level:
-        qs["fast"] = (replace(p, pbs_base_log=p.pbs_fast_base_log, pbs_level=p.pbs_fast_level),
-                      2 if p.pbs_fast_group == 2 else 1)
-    if p.pbs_fast2_level:
-        qs["fast2"] = (replace(p, pbs_base_log=p.pbs_fast2_base_log, pbs_level=p.pbs_fast2_level),
-                       2 if p.pbs_fast2_group == 2 else 1)
+    from fheicp.params import gadget_level, gadget_of
+    qs = {}
+    for g, gid in (("main", 0), ("mid", 3), ("mid2", 4), ("fast", 1), ("fast2", 2)):
+        if gid == 0 or gadget_level(p, gid):
+            bl, lv, grp = gadget_of(p, gid)
+            qs[g] = (replace(p, pbs_base_log=bl, pbs_level=lv), grp)
     pmc = load_pmc()
     ks = {g: _br_kernel(q, brs[g], pmc, grp) for g, (q, grp) in qs.items() if brs[g]["launches"]}
     dom = max(ks, key=lambda g: ks[g]["total_ms"])

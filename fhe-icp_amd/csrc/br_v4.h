@@ -377,16 +377,17 @@ struct Acc<false> {
   // and bits(r * 2^32 + 1.5 * 2^52) = bits(1.5 * 2^52) + rint(r * 2^32).
   // 8 f64 + 4 integer ops against f64_to_torus's 9 + 6 (split via floor,
   // a sign fix-up and two conversions).
-  static __device__ __forceinline__ T from_f64(double z) {
+  // (+ add: a constant folded into the subtraction, the A48 rounding bias)
+  static __device__ __forceinline__ T from_f64(double z, uint32_t add = 0) {
 #ifdef FHEICP_TORUS_SPLIT  // A/B build only (tools/build_variant.sh)
-    return f64_to_torus(__builtin_ldexp(z, 64));
+    return f64_to_torus(__builtin_ldexp(z, 64)) + add;
 #endif
     constexpr double M = 6755399441055744.0;
     const double F = __builtin_ldexp(z - __builtin_rint(z), 32);
     const double t1 = F + M;
     const double t2 = __builtin_ldexp(F - (t1 - M), 32) + M;
     const u64 hi = (u64)(uint32_t)__builtin_bit_cast(u64, t1) << 32;
-    return hi + (__builtin_bit_cast(u64, t2) - 0x4338000000000000ull);
+    return hi + (__builtin_bit_cast(u64, t2) - (0x4338000000000000ull - add));
   }
 };
 

@@ -139,11 +139,14 @@ static int validate(const fhe_params* p, std::string& why) {
       (p->pbs_mid2_level && !p->pbs_mid_level)) {
     why = "mid2 pbs decomposition out of range (0, 0 for none; needs the mid gadget)"; return -1;
   }
-  for (int g = 1; g <= 2; ++g) {
-    const int grp = g == 1 ? p->pbs_fast_group : p->pbs_fast2_group;
-    const int L = g == 1 ? p->pbs_fast_level : p->pbs_fast2_level;
-    const int bl = g == 1 ? p->pbs_fast_base_log : p->pbs_fast2_base_log;
-    if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group must be 0, 1 or 2"; return -1; }
+  for (int g = 1; g <= 4; ++g) {
+    const int grp = g == 1 ? p->pbs_fast_group : g == 2 ? p->pbs_fast2_group : g == 3 ? p->pbs_mid_group
+                                                                                     : p->pbs_mid2_group;
+    const int L = g == 1 ? p->pbs_fast_level : g == 2 ? p->pbs_fast2_level : g == 3 ? p->pbs_mid_level
+                                                                                    : p->pbs_mid2_level;
+    const int bl = g == 1 ? p->pbs_fast_base_log : g == 2 ? p->pbs_fast2_base_log
+                                                          : g == 3 ? p->pbs_mid_base_log : p->pbs_mid2_base_log;
+    if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group / pbs_mid_group / pbs_mid2_group must be 0, 1 or 2"; return -1; }
     (void)bl;  // 32-bit accumulators when level <= 2 and level * base_log <= 31, else 64-bit (k_blind_rotate_mb64)
     if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 8)) {
       why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 8";
@@ -176,9 +179,10 @@ static int gadget_base_log(const fhe_params& p, int g) {
   }
   return 0;
 }
-// grouping factor of gadget g's blind rotation (only fast / fast2 can be 2)
+// grouping factor of gadget g's blind rotation (the main gadget is classic)
 static int gadget_group(const fhe_params& p, int g) {
-  const int v = g == 1 ? p.pbs_fast_group : g == 2 ? p.pbs_fast2_group : 1;
+  const int v = g == 1 ? p.pbs_fast_group : g == 2 ? p.pbs_fast2_group : g == 3 ? p.pbs_mid_group
+                                                                               : g == 4 ? p.pbs_mid2_group : 1;
   return v == 2 ? 2 : 1;
 }
 
@@ -541,10 +545,13 @@ size_t fhe_fast_bsk_words(const fhe_params* p, int32_t which) {
   return fast_bsk_words(*p, which);
 }
 // the other gadgets' keys under the ChaCha20 streams 9/10 (fast), 11/12
-// (fast2), 17/18 (mid) and 19/20 (mid2); 13/14 and 15/16 for the fast
-// gadgets' multi-bit keys, whose GGSW messages k_mb_msgs derives
+// (fast2), 17/18 (mid) and 19/20 (mid2); 13/14, 15/16, 21/22 and 23/24 for
+// the fast, fast2, mid and mid2 gadgets' multi-bit keys, whose GGSW messages
+// k_mb_msgs derives
 static const uint32_t kTagMask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK};
 static const uint32_t kTagNoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE};
+static const uint32_t kTagMbMask[NGAD] = {0, TAG_MB2_MASK, TAG_MB3_MASK, TAG_MB4_MASK, TAG_MB5_MASK};
+static const uint32_t kTagMbNoise[NGAD] = {0, TAG_MB2_NOISE, TAG_MB3_NOISE, TAG_MB4_NOISE, TAG_MB5_NOISE};
 static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
   const fhe_params& p = ctx->p;
   const size_t shm = 8 * (size_t)p.N + p.N;
@@ -556,8 +563,7 @@ static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
     hipLaunchKernelGGL(k_keygen_bsk, dim3(fast_ggsws(p, g) * (q.k + 1) * q.pbs_level), dim3(256), shm, st, K, q.N,
                        q.k, q.pbs_level, q.pbs_base_log, q.glwe_noise_bits, mb ? ctx->mb_msg : ctx->s_small,
                        ctx->s_big, ctx->bskf[g - 1],
-                       mb ? (uint32_t)(g == 1 ? TAG_MB2_MASK : TAG_MB3_MASK) : kTagMask[g],
-                       mb ? (uint32_t)(g == 1 ? TAG_MB2_NOISE : TAG_MB3_NOISE) : kTagNoise[g]);
+                       mb ? kTagMbMask[g] : kTagMask[g], mb ? kTagMbNoise[g] : kTagNoise[g]);
   }
 }
 static int alloc_keys(fhe_ctx* ctx) {

@@ -3,6 +3,8 @@
 // Part of libfheicp (one translation unit: fheicp.hip includes it).
 #pragma once
 
+#include <type_traits>
+
 #include "common.h"
 #include "br_m512.h"
 #ifdef FHEICP_AB
@@ -708,20 +710,28 @@ __host__ __device__ constexpr int psi_pos(int x) { return x ^ ((x >> 4) & 15); }
 // which folds the digit shifts and widths into inline operands; 0 = `beta`.
 // Key rows come through buffer loads: a per-lane offset fixed for the kernel
 // and a scalar offset per row, so the loads take no VALU address arithmetic.
-// A32: 32-bit accumulators (L * beta <= 31, k_blind_rotate_mb); else 64-bit
-// ones (k_blind_rotate_mb64, the deep gadgets): the accumulator words are u64
-// with v4s's two-word rounding, and from L = 3 the level loop stays rolled and
-// each level's digits are read from the accumulator plus the rounding and
-// balancing offset (decompose_v4's offset form) instead of being kept.
-template <int L, int DBG, int BETA, bool A32>
+// AW = 1: 32-bit accumulators (L * beta <= 31, k_blind_rotate_mb); else wide
+// ones (k_blind_rotate_mb64, the deep gadgets) that carry the rounding and
+// balancing offset coff of decompose_v4's offset form from the start, so each
+// level's digits are plain bit fields of the accumulator word (minus B/2),
+// read when the level starts; the level loop is rolled from L = 3:
+// AW = 0 u64 words with v4s's two-word rounding; AW = 2 48-bit words, the
+// high 32 bits in acc[] and bits 16-31 of acc[u] and acc[u + S] packed in
+// alo[u] (24 VGPRs instead of 32), each product rounded into them at 2^-48
+// (n (1 + kN/2) 2^-96 / 12 = 2^-80 of variance, below the FFT error).
+template <int L, int DBG, int BETA, int AW>
 __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t count, int n, int beta,
                                           const c64* __restrict__ bsk, const c64* __restrict__ tw4,
                                           const c64* __restrict__ psi, BrTv tv, int mode, u64* __restrict__ out,
                                           u64* __restrict__ ct_v, u64* __restrict__ refreshed, u64* __restrict__ sign) {
   using namespace v4;
+  constexpr bool A32 = AW == 1, A48 = AW == 2;
   using AT = Acc<A32>;
-  using T = typename AT::T;
-  constexpr bool ROLL = !A32 && L >= 3;
+  using T = std::conditional_t<A48, uint32_t, typename AT::T>;
+#ifndef FHEICP_MB64_ROLL
+#define FHEICP_MB64_ROLL 99  // fully unrolled (rolled from L: A/B builds)
+#endif
+  constexpr bool ROLL = !A32 && L >= FHEICP_MB64_ROLL;
   constexpr int G = 4, NT = nthreads(G), NPSI = 2 * N;
   constexpr int OFF_TW = NPSI, OFF_X = OFF_TW + NTW, NC64 = OFF_X + G * WPC * SCR;
   __shared__ c64 lds[NC64];
@@ -734,7 +744,8 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   const int g = w / WPC, comp = w - g * WPC;
   const int64_t c = (int64_t)blockIdx.x * G + g;
   c64* slot = xbuf + (g * WPC + comp) * SCR;
-  T* sa = reinterpret_cast<T*>(slot);
+  using TS = std::conditional_t<A48, u64, T>;
+  TS* sa = reinterpret_cast<TS*>(slot);
   const int np = (n + 1) >> 1;
   const int bta = BETA ? BETA : beta;
   const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)bsk, (short)0, 0x7fffffff, 0x00020000);
@@ -770,28 +781,60 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   // this wave's product quarter: slots 2g, 2g+1 (uniform slot part of e)
   const uint32_t mq[2] = {(uint32_t)(256 * bitrev3(2 * g)), (uint32_t)(256 * bitrev3(2 * g + 1))};
 
-  T acc[2 * S];
-  {
-    const uint32_t bt = c < count ? modswitch_2n(small[(size_t)c * (n + 1) + n], 11) : 0;
-#pragma unroll
-    for (int s = 0; s < 2 * S; ++s) {
-      const uint32_t idx = (uint32_t)(s * 64 + lane + bt) & (2 * N - 1);
-      acc[s] = comp == K ? AT::from64(tv_rot(tv, idx, N)) : (T)0;
-    }
-  }
-
-  constexpr int R = WPC * L;  // GGSW rows per subset
-  // 64-bit accumulators: digit lv of word x is the plain beta-bit field of
-  // x + coff minus B/2 (decompose_v4's offset form, the same digits)
+  // the offset of decompose_v4's offset form (wide accumulators carry it)
   const int prec = L * bta;
   u64 coff = 0;
   if constexpr (!A32) {
     coff = (u64)1 << (63 - prec);
     for (int l = 0; l < L; ++l) coff += (u64)1 << (64 - prec + l * bta + bta - 1);
   }
-  auto digit_at = [&](T x, int lv) -> double {
-    const u64 rr = (u64)x + coff;
-    return (double)((int)((uint32_t)(rr >> (64 - prec + (L - 1 - lv) * bta)) & ((1u << bta) - 1u)) -
+  T acc[2 * S];
+  uint32_t alo[A48 ? S : 1];
+  // the accumulator word s as u64 (A48: its bits 0-15 zero)
+  auto word = [&](int s) -> u64 {
+    if constexpr (A48)
+      return ((u64)acc[s] << 32) | (s < S ? alo[s] << 16 : alo[s - S] & 0xffff0000u);
+    else
+      return AT::to64(acc[s]);
+  };
+  // A48: words u and u + S from u64 values whose bits 0-15 are dropped
+  auto set48 = [&](int u, u64 a, u64 b) {
+    acc[u] = (uint32_t)(a >> 32);
+    acc[u + S] = (uint32_t)(b >> 32);
+    alo[u] = __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x07060302u);
+  };
+  {
+    const uint32_t bt = c < count ? modswitch_2n(small[(size_t)c * (n + 1) + n], 11) : 0;
+#pragma unroll
+    for (int s = 0; s < 2 * S; ++s) {
+      const uint32_t idx = (uint32_t)(s * 64 + lane + bt) & (2 * N - 1);
+      if constexpr (A48) {
+        if (s < S) {
+          const uint32_t idx2 = (uint32_t)((s + S) * 64 + lane + bt) & (2 * N - 1);
+          // the test vector (a multiple of 2^(64 - P)) plus coff: exact in 48 bits
+          set48(s, (comp == K ? tv_rot(tv, idx, N) : 0) + coff, (comp == K ? tv_rot(tv, idx2, N) : 0) + coff);
+        }
+      } else if constexpr (A32) {
+        acc[s] = comp == K ? AT::from64(tv_rot(tv, idx, N)) : (T)0;
+      } else {
+        acc[s] = (comp == K ? tv_rot(tv, idx, N) : 0) + coff;
+      }
+    }
+  }
+
+  constexpr int R = WPC * L;  // GGSW rows per subset
+  // wide accumulators: digit lv of word x is the plain beta-bit field of x
+  // (which carries coff) minus B/2
+  auto digit_at = [&](int s, int lv) -> double {
+    u64 w;
+    if constexpr (A48) {
+      uint32_t t = s < S ? alo[s] : alo[s - S];
+      asm volatile("" : "+v"(t));  // unpacked per level, not hoisted out of the loop as 8 more VGPRs
+      w = ((u64)acc[s] << 32) | (s < S ? t << 16 : t);  // bits 0-15 unused (fields start >= 16)
+    } else {
+      w = (u64)acc[s];
+    }
+    return (double)((int)((uint32_t)(w >> (64 - prec + (L - 1 - lv) * bta)) & ((1u << bta) - 1u)) -
                     (1 << (bta - 1)));
   };
   for (int j = 0; j < np; ++j) {
@@ -817,7 +860,7 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
 #pragma unroll
         for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
       } else {
-        v[s] = {digit_at(acc[s], 0), digit_at(acc[s + S], 0)};
+        v[s] = {digit_at(s, 0), digit_at(s + S, 0)};
       }
     }
     V4_STAMP(1);
@@ -835,7 +878,7 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
           if constexpr (A32)
             v[u] = {(double)(int16_t)(dg[lv - 1][u] & 0xffff), (double)((int32_t)dg[lv - 1][u] >> 16)};
           else
-            v[u] = {digit_at(acc[u], lv), digit_at(acc[u + S], lv)};
+            v[u] = {digit_at(u, lv), digit_at(u + S, lv)};
         }
       }
       // key rows of this quarter, slot t: [subset][row] (9 per slot)
@@ -912,8 +955,13 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
     inverse<0, NR>(ov, twl, slot, lane, {}, treg);
 #pragma unroll
     for (int u = 0; u < S; ++u) {
-      acc[u] += AT::from_f64(ov[u].x);
-      acc[u + S] += AT::from_f64(ov[u].y);
+      if constexpr (A48) {
+        // + 2^15: the truncation to 48 bits rounds to nearest
+        set48(u, word(u) + Acc<false>::from_f64(ov[u].x, 0x8000u), word(u + S) + Acc<false>::from_f64(ov[u].y, 0x8000u));
+      } else {
+        acc[u] += AT::from_f64(ov[u].x);
+        acc[u + S] += AT::from_f64(ov[u].y);
+      }
     }
     MB_PRIO(br_prio_fine<L>() ? 2 : 0);
     V4_STAMP(11);
@@ -927,8 +975,19 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   }
 
   // sample extraction of coefficient 0 (as k_blind_rotate_v4)
+  auto sword = [&](int i) -> u64 {
+    if constexpr (A48)
+      return sa[i] - coff;
+    else
+      return AT::to64(sa[i]) - coff;
+  };
 #pragma unroll
-  for (int s = 0; s < 2 * S; ++s) sa[s * 64 + lane] = acc[s];
+  for (int s = 0; s < 2 * S; ++s) {
+    if constexpr (A48)
+      sa[s * 64 + lane] = word(s);
+    else
+      sa[s * 64 + lane] = acc[s];
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (c < count) {
     const int W = K * N + 1;
@@ -936,11 +995,11 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
 #pragma unroll
       for (int s = 0; s < 2 * S; ++s) {
         const int t = s * 64 + lane;
-        const u64 x = t == 0 ? AT::to64(sa[0]) : (u64)0 - AT::to64(sa[N - t]);
+        const u64 x = t == 0 ? sword(0) : (u64)0 - sword(N - t);
         br_emit(mode, x, false, tv, (size_t)c * W + comp * N + t, out, ct_v, refreshed, sign);
       }
     } else if (lane == 0) {
-      br_emit(mode, AT::to64(acc[0]), true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
+      br_emit(mode, word(0) - coff, true, tv, (size_t)c * W + K * N, out, ct_v, refreshed, sign);
     }
   }
 }
@@ -952,9 +1011,13 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u6
                                                                       const c64* __restrict__ psi, BrTv tv, int mode,
                                                                       u64* __restrict__ out, u64* __restrict__ ct_v,
                                                                       u64* __restrict__ refreshed, u64* __restrict__ sign) {
-  mb_rotate<L, DBG, BETA, true>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
+  mb_rotate<L, DBG, BETA, 1>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
 }
-// the deep gadgets (L * beta > 31) on the multi-bit rotation: 64-bit accumulators
+// the deep gadgets (L * beta > 31) on the multi-bit rotation: 48-bit accumulators
+// (FHEICP_MB64_AW = 0: 64-bit ones, A/B builds)
+#ifndef FHEICP_MB64_AW
+#define FHEICP_MB64_AW 2
+#endif
 template <int L, int DBG = 0>
 __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb64(const u64* __restrict__ small, int64_t count,
                                                                         int n, int beta, const c64* __restrict__ bsk,
@@ -963,7 +1026,7 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb64(const 
                                                                         u64* __restrict__ out, u64* __restrict__ ct_v,
                                                                         u64* __restrict__ refreshed,
                                                                         u64* __restrict__ sign) {
-  mb_rotate<L, DBG, 0, false>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
+  mb_rotate<L, DBG, 0, FHEICP_MB64_AW>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
 }
 
 // ---- classic blind rotation with key-stationary products ---------------------

@@ -33,6 +33,10 @@ enum StreamTag : uint32_t {
   TAG_BSK4_NOISE = 18,
   TAG_BSK5_MASK = 19,  // the mid2 gadget's bootstrapping key (fhe_params.pbs_mid2_*)
   TAG_BSK5_NOISE = 20,
+  TAG_MB4_MASK = 21,   // the mid gadget's multi-bit key (fhe_params.pbs_mid_group = 2)
+  TAG_MB4_NOISE = 22,
+  TAG_MB5_MASK = 23,   // the mid2 gadget's multi-bit key
+  TAG_MB5_NOISE = 24,
 };
 
 struct ChaKey {

@@ -57,6 +57,10 @@ class SchemeParams:
     pbs_mid_level: int = 0
     pbs_mid2_base_log: int = 0
     pbs_mid2_level: int = 0
+    # grouping factor of the mid / mid2 gadget's blind rotation (as
+    # pbs_fast_group; 2 = multi-bit, 64-bit accumulators past level 2)
+    pbs_mid_group: int = 0
+    pbs_mid2_group: int = 0
 
     def as_dict(self) -> dict:
         return asdict(self)
@@ -77,14 +81,16 @@ SIGMA_BAR = 9.2
 # candidate fast gadgets for the low-amplification sign rounds, each with
 # the classic (1) or the multi-bit (2) blind rotation, and the blind-rotation
 # time per bootstrap by (level, group) relative to L = 2 classic, measured on
-# MI355X at 1024 ciphertexts (tools/prof_br.py --gadget, tools/deep_ab.sh,
-# tools/lib_ab.sh): classic v4 (32-bit accumulators) L = 1, 2: 6.0 / 9.45 ms;
-# key-stationary v4s (64-bit) L = 3..8: 16.0 / 19.6 / 23.0 / 26.4 / 29.5 /
-# 32.8 ms (prof_br times, 11.2 ms at L = 2 classic); multi-bit L = 1, 2:
-# 4.0 / 6.7 ms. Only the ranking matters.
+# MI355X at 4096 ciphertexts (tests/test_gpu_noise.py timing lines,
+# profiles/r03e_noise.log), ms per 1024: classic v4 (32-bit accumulators)
+# L = 1, 2: 6.38 / 9.87; key-stationary v4s (64-bit) L = 3..8: 13.9 / 18.0 /
+# 21.0 / 24.4 / 27.4 / 31.1; multi-bit L = 1, 2 (32-bit): 4.32 / 7.09; multi-bit
+# L = 3..8 (48-bit, mb64): 10.5 / 13.0 / 15.9 / 18.6 / 21.4 / 24.2. Only the
+# ranking matters.
 FAST_GADGETS = ((15, 2, 1), (23, 1, 1), (15, 2, 2), (23, 1, 2))
-BR_COST = {(1, 1): 0.61, (2, 1): 1.0, (3, 1): 1.43, (4, 1): 1.75, (5, 1): 2.05, (6, 1): 2.35, (7, 1): 2.63,
-           (8, 1): 2.92, (1, 2): 0.41, (2, 2): 0.69}
+BR_COST = {(1, 1): 0.647, (2, 1): 1.0, (3, 1): 1.413, (4, 1): 1.824, (5, 1): 2.125, (6, 1): 2.476,
+           (7, 1): 2.781, (8, 1): 3.147, (1, 2): 0.438, (2, 2): 0.718, (3, 2): 1.059, (4, 2): 1.313,
+           (5, 2): 1.612, (6, 2): 1.884, (7, 2): 2.164, (8, 2): 2.454}
 
 
 def sign_rounds(P: int, d: int):
@@ -123,9 +129,9 @@ def gadget_of(p: "SchemeParams", g: int):
     if g in (1, 2) and p.pbs_fast_level:
         return p.pbs_fast_base_log, p.pbs_fast_level, max(p.pbs_fast_group, 1)
     if g == 3 and p.pbs_mid_level:
-        return p.pbs_mid_base_log, p.pbs_mid_level, 1
+        return p.pbs_mid_base_log, p.pbs_mid_level, max(p.pbs_mid_group, 1)
     if g == 4 and p.pbs_mid2_level:
-        return p.pbs_mid2_base_log, p.pbs_mid2_level, 1
+        return p.pbs_mid2_base_log, p.pbs_mid2_level, max(p.pbs_mid2_group, 1)
     return p.pbs_base_log, p.pbs_level, 1
 
 
@@ -274,14 +280,17 @@ def _cheapest_plan(p: SchemeParams) -> SchemeParams:
         if c < best - 1e-9:
             p, best = q, c
     if p.pbs_fast_level:
-        # then one or two mid gadgets: cheaper main gadgets of PBS_GADGETS,
-        # between the main and the fast one
-        mids = [(b, lv) for _, b, lv in PBS_GADGETS if lv < lvl]
+        # then one or two mid gadgets between the main and the fast one:
+        # gadgets of PBS_GADGETS on the classic rotation below the main level,
+        # or on the multi-bit one at any level up to it (a multi-bit mid at the
+        # main gadget's own level can take the first rounds from it)
+        mids = [(b, lv, 1) for _, b, lv in PBS_GADGETS if lv < lvl]
+        mids += [(b, lv, 2) for _, b, lv in PBS_GADGETS if 3 <= lv <= lvl and (lv, 2) in BR_COST]
         q0 = p
         for ch in [(m,) for m in mids] + [(a, b) for a in mids for b in mids if a[1] > b[1]]:
-            kw = {"pbs_mid_base_log": ch[0][0], "pbs_mid_level": ch[0][1]}
+            kw = {"pbs_mid_base_log": ch[0][0], "pbs_mid_level": ch[0][1], "pbs_mid_group": ch[0][2]}
             if len(ch) > 1:
-                kw.update(pbs_mid2_base_log=ch[1][0], pbs_mid2_level=ch[1][1])
+                kw.update(pbs_mid2_base_log=ch[1][0], pbs_mid2_level=ch[1][1], pbs_mid2_group=ch[1][2])
             q = replace(q0, **kw)
             c = plan_cost(q)
             if c < best - 1e-9:

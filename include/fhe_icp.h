@@ -70,8 +70,8 @@ typedef struct fhe_params {
   int32_t pbs_fast2_group; /* rotation: 0 or 1 = classic, one LWE coefficient per step;
                               2 = multi-bit, pairs of coefficients with three GGSWs
                               each (fhe_export_fast_bsk's layout: [pair][subset][row]
-                              [component][coef]); needs N = 1024, k = 2, level <= 2,
-                              level * base_log <= 31 */
+                              [component][coef]); needs N = 1024, k = 2, n <= 1023,
+                              level <= 8 */
   int32_t pbs_mid_base_log;  /* optional gadgets between the main and the fast one */
   int32_t pbs_mid_level;     /* (0, 0: none; classic rotation; mid needs the fast  */
   int32_t pbs_mid2_base_log; /* gadget, mid2 needs mid): the sign plan runs the     */
@@ -79,6 +79,10 @@ typedef struct fhe_params {
                                 gadget on the fewest rounds that keep every decision
                                 at 9.2 sigma (fhe_sign_schedule).
                                 Their keys: fhe_export_fast_bsk which = 3, 4. */
+  int32_t pbs_mid_group;     /* grouping factor of the mid / mid2 gadget's blind */
+  int32_t pbs_mid2_group;    /* rotation, as pbs_fast_group: 2 = multi-bit (levels
+                                up to 8; 64-bit accumulators past level 2 or
+                                level * base_log > 31: k_blind_rotate_mb64) */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;

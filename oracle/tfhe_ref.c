@@ -55,6 +55,8 @@ typedef struct {
   int32_t pbs_mid_level;      /* (classic rotation; 0, 0 = none; mid needs  */
   int32_t pbs_mid2_base_log;  /* the fast gadget, mid2 needs mid)           */
   int32_t pbs_mid2_level;
+  int32_t pbs_mid_group;      /* blind rotation of the mid / mid2 gadget    */
+  int32_t pbs_mid2_group;     /* (as pbs_fast_group)                        */
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -135,7 +137,8 @@ int64_t ref_tuniform(uint64_t w, int b) { return tuniform(w, b); }
 enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, TAG_KSK_MASK = 5,
        TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10,
        TAG_BSK3_MASK = 11, TAG_BSK3_NOISE = 12, TAG_MB2_MASK = 13, TAG_MB2_NOISE = 14, TAG_MB3_MASK = 15,
-       TAG_MB3_NOISE = 16, TAG_BSK4_MASK = 17, TAG_BSK4_NOISE = 18, TAG_BSK5_MASK = 19, TAG_BSK5_NOISE = 20 };
+       TAG_MB3_NOISE = 16, TAG_BSK4_MASK = 17, TAG_BSK4_NOISE = 18, TAG_BSK5_MASK = 19, TAG_BSK5_NOISE = 20,
+       TAG_MB4_MASK = 21, TAG_MB4_NOISE = 22, TAG_MB5_MASK = 23, TAG_MB5_NOISE = 24 };
 
 /* --------------------------------------------------- negacyclic product --- */
 /* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
@@ -221,7 +224,8 @@ static void bsk_gen(const ref_params* P, const ref_key* Kp, int beta, int L, int
  * pairs (s1, s2) = (s[2j], s[2j+1]), s2 = 0 past n; pair j has three GGSWs,
  * of s1(1-s2), (1-s1)s2 and s1 s2 (the subsets {1}, {2}, {1,2}). */
 static int gadget_group(const ref_params* P, int which) {
-  const int g = which == 1 ? P->pbs_fast_group : which == 2 ? P->pbs_fast2_group : 1;
+  const int g = which == 1 ? P->pbs_fast_group : which == 2 ? P->pbs_fast2_group
+              : which == 3 ? P->pbs_mid_group : which == 4 ? P->pbs_mid2_group : 1;
   return g == 2 ? 2 : 1;
 }
 /* gadget `which`: 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2 (level 0: absent) */
@@ -277,8 +281,9 @@ int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uin
   if (gadget_group(P, which) == 2) {
     uint64_t* msg = (uint64_t*)malloc(8 * 3 * (size_t)npairs(P));
     mb_msgs(P, s_small, msg);
-    bsk_gen(P, &K, bl, L, which == 1 ? TAG_MB2_MASK : TAG_MB3_MASK, which == 1 ? TAG_MB2_NOISE : TAG_MB3_NOISE, msg,
-            3 * npairs(P), s_big, bsk2);
+    static const int mmask[NGAD] = {0, TAG_MB2_MASK, TAG_MB3_MASK, TAG_MB4_MASK, TAG_MB5_MASK};
+    static const int mnoise[NGAD] = {0, TAG_MB2_NOISE, TAG_MB3_NOISE, TAG_MB4_NOISE, TAG_MB5_NOISE};
+    bsk_gen(P, &K, bl, L, mmask[which], mnoise[which], msg, 3 * npairs(P), s_big, bsk2);
     free(msg);
   } else {
     bsk_gen(P, &K, bl, L, tmask[which], tnoise[which], s_small, P->n, s_big, bsk2);
@@ -955,8 +960,8 @@ void ref_sign_extract_keys(const ref_params* P0, const uint64_t* bsk, const uint
   ref_params Pm = *P0;
   if (!keys[0]) Pm.pbs_fast_base_log = Pm.pbs_fast_level = Pm.pbs_fast_group = 0;
   if (!keys[0] || !keys[1]) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = Pm.pbs_fast2_group = 0;
-  if (!keys[0] || !keys[2]) Pm.pbs_mid_base_log = Pm.pbs_mid_level = 0;
-  if (!Pm.pbs_mid_level || !keys[3]) Pm.pbs_mid2_base_log = Pm.pbs_mid2_level = 0;
+  if (!keys[0] || !keys[2]) Pm.pbs_mid_base_log = Pm.pbs_mid_level = Pm.pbs_mid_group = 0;
+  if (!Pm.pbs_mid_level || !keys[3]) Pm.pbs_mid2_base_log = Pm.pbs_mid2_level = Pm.pbs_mid2_group = 0;
   const ref_params* P = &Pm;
   const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
   gadget_sched g0;

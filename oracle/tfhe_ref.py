@@ -19,7 +19,7 @@ FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
           "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
           "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
           "pbs_fast_group", "pbs_fast2_group", "pbs_mid_base_log", "pbs_mid_level", "pbs_mid2_base_log",
-          "pbs_mid2_level")
+          "pbs_mid2_level", "pbs_mid_group", "pbs_mid2_group")
 OPTIONAL = FIELDS[FIELDS.index("sign_digit_bits"):]
 # gadget g = 1..4 (fast, fast2, mid, mid2) and the level field that enables it
 GADGET_LEVEL = {1: "pbs_fast_level", 2: "pbs_fast2_level", 3: "pbs_mid_level", 4: "pbs_mid2_level"}

@@ -8,7 +8,7 @@ from pathlib import Path
 import pytest
 
 from fheicp import _lib
-from fheicp.params import TOY, params_for_bits
+from fheicp.params import TOY, params_for_bits, sign_plan
 
 INCLUDE = Path(__file__).resolve().parents[1] / "include"
 HEADERS = sorted(INCLUDE.glob("*.h"))       # fhe_icp.h (the compare path), fhe_bert.h (§8 f4)
@@ -95,7 +95,10 @@ def test_fast_gadget_validation_and_host_calls():
     P = _lib.params_struct(base)
     assert L.fhe_sign_plan(C.byref(P), None, None, None) == 0
     j1 = C.c_int32()
-    assert L.fhe_sign_plan(C.byref(P), None, C.byref(j1), None) == 0 and j1.value == 1
+    # P = 19: a multi-bit mid gadget at the main gadget's level takes the
+    # first round, so the main gadget runs none (params.sign_plan agrees)
+    assert L.fhe_sign_plan(C.byref(P), None, C.byref(j1), None) == 0
+    assert j1.value == sign_plan(params_for_bits(19))[1] == 0
     assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
     buf = (C.c_uint64 * 1)()
     assert L.fhe_export_fast_bsk(h, 1, buf) == -2

@@ -7,7 +7,8 @@ DESIGN.md §3.5). Sampling a thousand compares cannot show that, so for each
 kernel instance the parameter table can select (v4 32-bit accumulators at
 (15,2) and (23,1), the key-stationary v4s with 64-bit accumulators at (12,3)
 and levels 4..8, and the multi-bit rotation of the fast gadgets at (15,2)
-and (23,1), plus its run-time-base-log instances) this measures the output noise of >= 4096 bootstraps on the real
+and (23,1), plus its run-time-base-log instances, and the deep gadgets on
+the multi-bit rotation with 48-bit accumulators) this measures the output noise of >= 4096 bootstraps on the real
 parameters and checks it against the model (fheicp.params._variances, the
 same formula as fheicp.hip and oracle/tfhe_ref.c), and checks a few output
 phases against the exact oracle's bootstrap of the same inputs.
@@ -44,10 +45,13 @@ INSTANCES = {
     # the multi-bit kernels with a run-time base log (other gadgets)
     (14, 2, 2): "k_blind_rotate_mb<2, 0, 0>",
     (22, 1, 2): "k_blind_rotate_mb<1, 0, 0>",
-    # the deep gadgets on the multi-bit rotation, 64-bit accumulators
+    # the deep gadgets on the multi-bit rotation, 48-bit accumulators
     (12, 3, 2): "k_blind_rotate_mb64<3, 0>",
     (10, 4, 2): "k_blind_rotate_mb64<4, 0>",
     (8, 5, 2): "k_blind_rotate_mb64<5, 0>",
+    (7, 6, 2): "k_blind_rotate_mb64<6, 0>",
+    (6, 7, 2): "k_blind_rotate_mb64<7, 0>",
+    (5, 8, 2): "k_blind_rotate_mb64<8, 0>",
 }
 COUNT = 4096
 TV = 1 << 61

@@ -227,10 +227,11 @@ TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_leve
 @pytest.mark.parametrize("P,grp", [(8, 1), (16, 2), (16, 1), (19, 2), (26, 2)])
 def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
     """Every bootstrapping key of a multi-gadget parameter set (toy (12,3)+(8,2);
-    real P=16: (15,2) + (15,2) + (23,1); P=19: (12,3) + (15,2) + (23,1); P=26:
-    (6,7) + mid (8,5) + mid2 (12,3) + (15,2) + (23,1)) is bit-exact against
-    the oracle's keygen, the fast gadgets' keys as multi-bit keys (group 2:
-    three GGSWs per pair) and as classic ones."""
+    real P=16: (15,2) + (15,2) + (23,1); P=19: (12,3) + mid (12,3) + (15,2) +
+    (23,1); P=26: (5,8) + mid (8,5) + mid2 (12,3) + (15,2) + (23,1)) is
+    bit-exact against the oracle's keygen, the fast gadgets' keys as
+    multi-bit keys (group 2: three GGSWs per pair) and as classic ones, the
+    mid gadgets' as the planner sets them (multi-bit)."""
     prm = replace(TOY, msg_bits=P, **TOY_FAST) if P < 12 else params_for_bits(P)
     if P >= 12:
         prm = replace(prm, pbs_fast_group=grp, pbs_fast2_group=grp)
@@ -245,7 +246,7 @@ def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
     for which in (3, 4):
         if which in ref.keys:
             assert np.array_equal(eng.export_fast_bsk(which), ref.keys[which]), which
-    assert (3 in ref.keys) == (P == 26)
+    assert (3 in ref.keys) == (P >= 17)   # multi-bit mid keys (tags 21-24) from P = 17
     eng.close()
 
 

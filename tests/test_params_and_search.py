@@ -81,8 +81,7 @@ def test_fast_gadget_plan():
     from fheicp.params import _plan_worst, plan_cost
     F, F2 = (15, 2, 2), (23, 1, 2)
     want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F, F2, (4, 0, 1)), 12: (F, F2, (4, 0, 1)),
-            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 0, 3)), 17: (F, F2, (4, 1, 5)), 18: (F, F2, (4, 1, 5)),
-            19: (F, F2, (4, 1, 5)), 20: (F, F2, (4, 2, 5))}
+            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 0, 3))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
         assert p.pbs_mid_level == 0, P
@@ -101,23 +100,30 @@ def test_fast_gadget_plan():
     # multi-bit form, four on multi-bit (23,1)
     assert sign_plan(params_for_bits(16)) == (4, 0, 3)
     assert sign_plan(params_for_bits(19, fast=False)) == (4, 9, 9)
+    # from P = 17 a mid gadget joins (test_mid_gadget_plan)
+    assert params_for_bits(17).pbs_mid_level
     assert params_for_bits(3).pbs_fast_level == 0
 
 
 def test_mid_gadget_plan():
-    """Mid gadgets: from P = 21 the plan adds one or two
-    cheaper main gadgets between the main and the fast one. The schedule walks
-    main -> mid -> mid2 -> fast -> fast2, each gadget on the fewest rounds for
-    which the next one on all the rest keeps every decision at 9.2 sigma, and
-    the plan is cheaper than the same gadgets without mids."""
+    """Mid gadgets: from P = 17 the plan adds one or two
+    gadgets between the main and the fast one, on the multi-bit rotation with
+    48-bit accumulators (k_blind_rotate_mb64), 0.72-0.78x the classic time at
+    the same gadget (BR_COST, measured). The schedule walks main -> mid -> mid2
+    -> fast -> fast2, each gadget on the fewest rounds for which the next one
+    on all the rest keeps every decision at 9.2 sigma, and the plan is cheaper
+    than the same gadgets without mids. A multi-bit mid at the main gadget's
+    own level takes the first round wherever its (3x key) noise allows."""
     from dataclasses import replace
     from fheicp.params import _sched_worst, plan_cost, sign_schedule
-    want = {21: ((12, 3), None), 22: ((12, 3), None), 23: ((12, 3), None),
-            24: ((10, 4), (12, 3)), 25: ((10, 4), (12, 3)), 26: ((8, 5), (12, 3)), 27: ((8, 5), (12, 3))}
+    M3, M4, M5, M6 = (12, 3, 2), (10, 4, 2), (8, 5, 2), (7, 6, 2)
+    want = {17: (M3, None), 19: (M3, None), 20: (M4, M3), 21: (M4, M3), 22: (M5, M3), 23: (M5, M4),
+            24: (M4, M3), 25: (M5, M3), 26: (M5, M3), 27: (M6, M4)}
     for P, (m1, m2) in want.items():
         p = params_for_bits(P)
-        assert (p.pbs_mid_base_log, p.pbs_mid_level) == m1, P
-        assert ((p.pbs_mid2_base_log, p.pbs_mid2_level) if p.pbs_mid2_level else None) == m2, P
+        assert (p.pbs_mid_base_log, p.pbs_mid_level, p.pbs_mid_group) == m1, P
+        got2 = (p.pbs_mid2_base_log, p.pbs_mid2_level, p.pbs_mid2_group) if p.pbs_mid2_level else None
+        assert got2 == m2, P
         d, sched = sign_schedule(p)
         assert len(sched) == sign_pbs_count(p) and _sched_worst(p, d, sched) >= 9.2, P
         lad = [g for g in (0, 3, 4, 1, 2) if g in sched]
@@ -128,9 +134,13 @@ def test_mid_gadget_plan():
             if c > start:
                 fewer = sched[:c - 1] + [lad[i + 1]] * (len(sched) - c + 1)
                 assert _sched_worst(p, d, fewer) < 9.2, (P, i)
-        nomid = replace(p, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid2_base_log=0, pbs_mid2_level=0)
+        nomid = replace(p, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid2_base_log=0, pbs_mid2_level=0,
+                        pbs_mid_group=0, pbs_mid2_group=0)
         assert plan_cost(p) < plan_cost(nomid), P
-    # C5's width: 1 main (5,8), 2 mid (8,5), 2 mid2 (12,3), 4 fast, 4 fast2
+        classic = replace(p, pbs_mid_group=0, pbs_mid2_group=0)
+        assert plan_cost(p) < plan_cost(classic), P
+    # C5's width: 1 main (5,8) classic, 2 mid (8,5) and 2 mid2 (12,3) multi-bit,
+    # 4 fast, 4 fast2
     p26 = params_for_bits(26)
     assert (p26.pbs_base_log, p26.pbs_level, p26.pbs_mid_base_log, p26.pbs_mid_level,
             p26.pbs_mid2_base_log, p26.pbs_mid2_level) == (5, 8, 8, 5, 12, 3)
@@ -138,13 +148,14 @@ def test_mid_gadget_plan():
     # the headline width runs every round on the multi-bit fast gadgets: the
     # main (15, 2) key is made but never launched
     assert sign_schedule(params_for_bits(16))[1] == [1, 1, 1, 2, 2, 2, 2]
-    # the headline width has no mid gadget; C3's (P = 21) takes the more
-    # precise (10,4) main gadget, whose quieter first bootstrap allows 4-bit
-    # digits: 10 bootstraps instead of 13
+    # the headline width has no mid gadget; C3's (P = 21) takes the (10,4)
+    # gadget, whose quieter first bootstrap allows 4-bit digits (10 bootstraps
+    # instead of 13), on the multi-bit rotation for its first round (the
+    # classic (10,4) main key is made, never launched), then 2 x mb (12,3)
     assert params_for_bits(16).pbs_mid_level == 0
     p21 = params_for_bits(21)
     assert (p21.pbs_base_log, p21.pbs_level) == (10, 4)
-    assert sign_schedule(p21) == (4, [0, 3, 3, 1, 1, 1, 1, 2, 2, 2])
+    assert sign_schedule(p21) == (4, [3, 4, 4, 1, 1, 1, 1, 2, 2, 2])
 
 
 def test_multibit_noise_model():
