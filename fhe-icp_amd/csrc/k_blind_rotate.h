@@ -777,9 +777,10 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
     atab[jj][gg] = a1 | (a2 << 16);
   }
   __syncthreads();
-  const uint32_t ebase = (uint32_t)mb::exponent(lane, 0);
-  // this wave's product quarter: slots 2g, 2g+1 (uniform slot part of e)
-  const uint32_t mq[2] = {(uint32_t)(256 * bitrev3(2 * g)), (uint32_t)(256 * bitrev3(2 * g + 1))};
+  // this wave's product quarter: slots 2g, 2g+1; the exponent of slot 2g in
+  // 16-byte units, so a * eb16 holds the table entry's byte offset (before
+  // the swizzle) in bits 4-14
+  const uint32_t eb16 = (((uint32_t)mb::exponent(lane, 0) + 256u * bitrev3(2 * g)) & 2047u) << 4;
 
   // the offset of decompose_v4's offset form (wide accumulators carry it)
   const int prec = L * bta;
@@ -907,7 +908,7 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
       // bitrev3(2g) + 4): its table position is slot 2g's with bit 10
       // flipped when a is odd (the swizzle only reads bits 4-7), so the
       // address is computed once per (ciphertext, subset)
-      uint32_t pa[G][3];
+      uint32_t pa[G][3];  // byte offsets into the psi table
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         // the second slot's rows load when it starts: prefetching them with
@@ -928,12 +929,14 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
 #pragma unroll
             for (int r = 0; r < WPC; ++r) cmac(P, F[r], kb[t][Ss][r]);
             if (t == 0) {
-              const uint32_t x = (__umul24(aS[gg][Ss], ebase) + aS[gg][Ss] * mq[0]) & (2 * N - 1);
-              pa[gg][Ss] = (uint32_t)mb::psi_pos((int)x);
+              // 16 psi_pos(a e mod 2N) = X ^ ((X >> 4) & 0xf0), X = 16 (a e mod 2N)
+              const uint32_t pr = __umul24(aS[gg][Ss], eb16);
+              pa[gg][Ss] = (pr & 0x7ff0u) ^ ((pr >> 4) & 0xf0u);
             } else {
-              pa[gg][Ss] ^= (aS[gg][Ss] & 1u) << 10;
+              pa[gg][Ss] ^= (aS[gg][Ss] & 1u) << 14;
             }
-            cmac(o[gg][t], psil[pa[gg][Ss]], P);  // the table holds psi^x - 1
+            // the table holds psi^x - 1
+            cmac(o[gg][t], *reinterpret_cast<const c64*>(reinterpret_cast<const char*>(psil) + pa[gg][Ss]), P);
           }
         }
       }
