@@ -7,7 +7,8 @@
 # config merges into the same file (entries keyed kernel@cts); $PMC_ENV names
 # an environment prefix of the command in the record (e.g. "FHEICP_PIPE=0 ").
 set -u
-R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/pmc_bench; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=${PMC_OUT:-$R/gpurun_out/pmc_bench}; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
+rm -rf "$OUT/f64" "$OUT/fetch" "$OUT/write" "$OUT/trace"   # csvof reads the first file of each pass
 CMD="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}"
 csvof() { ls "$1"/*counter_collection.csv "$1"/*/*counter_collection.csv 2>/dev/null | head -n1; }
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU \
