@@ -27,47 +27,71 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---- GEMM: out[M][N] = A[M][K] . W[N][K]^T + bias (+ epilogue) ------------
-// 128 x 128 block tile, K step 64, 4 waves in 2 x 2, each a 64 x 64 tile of
-// 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators. Operands go global -> registers
-// -> LDS (double buffered, one barrier per K step); LDS rows are padded to 72
-// bf16 (144 B = 9 x 16 B), so the 16 lanes of a ds_read_b128 group (rows
-// l & 15) land on 16 distinct bank quads (9 r mod 16 is a permutation).
-constexpr int BM = 128, BN = 128, BK = 64, LDK = BK + 8;
-constexpr int GEMM_LDS = 2 * (BM + BN) * LDK * (int)sizeof(bf16);  // 73728 B
+// 256 x BN block tile (BN = 256, or 128 when N is small: more tiles than
+// CUs), K step 64, 8 waves of 512 threads in (8 / (BN/64)) x (BN/64), each a
+// (256 / waves_m) x 64 tile of 16 x 16 v_mfma_f32_16x16x32_bf16 accumulators
+// (8 x 4 at BN = 256: 0.375 LDS fragment reads per MFMA). Operands go
+// global -> registers -> LDS, double buffered: the next K step's loads are in
+// flight during this step's 64 MFMAs per wave, one barrier per K step. LDS
+// rows are padded to 72 bf16 (144 B = 9 x 16 B), so the 16 lanes of a
+// ds_read_b128 group (rows l & 15) land on 16 distinct bank quads (9 r mod 16
+// is a permutation). Tiles are numbered row-major and dealt XCD by XCD, so
+// the column tiles of one 256-row band (which share its A rows) run on one
+// XCD's L2.
+constexpr int BM = 256, BK = 64, LDK = BK + 8;
+template <int BN>
+constexpr int gemm_lds() { return 2 * (BM + BN) * LDK * (int)sizeof(bf16); }  // 147456 / 110592 B
 enum { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2 };
 
-template <int EPI>
-__global__ void __launch_bounds__(256) k_gemm(const bf16* __restrict__ A, const bf16* __restrict__ W,
+template <int EPI, int BN>
+__global__ void __launch_bounds__(512) k_gemm(const bf16* __restrict__ A, const bf16* __restrict__ W,
                                               const float* __restrict__ bias, const float* __restrict__ resid,
-                                              void* __restrict__ out, int M, int N, int K) {
+                                              void* __restrict__ out, int M, int N, int K, int tiles_n, int nblk) {
+  constexpr int WN = BN / 64, WM = 8 / WN;  // waves along N and M
+  constexpr int FM = BM / WM / 16;          // 16-row fragments per wave
+  constexpr int AL = BM * BK / 8 / 512, BL = BN * BK / 8 / 512;  // 16-byte loads per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* sa = reinterpret_cast<bf16*>(smem);   // [2][BM][LDK]
   bf16* sb = sa + 2 * BM * LDK;               // [2][BN][LDK]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int wm = w / WN, wn = w - wm * WN;
+  // XCD-aware tile order (bijective for any nblk): block b runs on XCD b % 8
+  const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * BN;
   const int KT = K / BK;
-  uint4 ra[4], rb[4];
+  uint4 ra[AL], rb[BL];
   auto load_regs = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, kc = (c & 7) * 8;
-      const int gm = m0 + row, gn = n0 + row, k = kt * BK + kc;
-      ra[i] = gm < M ? *reinterpret_cast<const uint4*>(A + (size_t)gm * K + k) : make_uint4(0, 0, 0, 0);
-      rb[i] = gn < N ? *reinterpret_cast<const uint4*>(W + (size_t)gn * K + k) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < AL; ++i) {
+      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
+      // (guarded loads: unguarded ones from a clamped row let the scheduler
+      // hoist every fragment read and spill the staging registers)
+      const int gm = m0 + row;
+      ra[i] = gm < M ? *reinterpret_cast<const uint4*>(A + (size_t)gm * K + kt * BK + kc) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
+      const int gn = n0 + row;
+      rb[i] = gn < N ? *reinterpret_cast<const uint4*>(W + (size_t)gn * K + kt * BK + kc) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_lds = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i, row = c >> 3, kc = (c & 7) * 8;
+    for (int i = 0; i < AL; ++i) {
+      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
       *reinterpret_cast<uint4*>(sa + (buf * BM + row) * LDK + kc) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
       *reinterpret_cast<uint4*>(sb + (buf * BN + row) * LDK + kc) = rb[i];
     }
   };
-  f32x4 acc[4][4];
+  f32x4 acc[FM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -77,45 +101,71 @@ __global__ void __launch_bounds__(256) k_gemm(const bf16* __restrict__ A, const 
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < KT) load_regs(kt + 1);  // in flight during the MFMAs
-    const bf16* ca = sa + (cur * BM + wm * 64 + (l & 15)) * LDK + 8 * (l >> 4);
+    const bf16* ca = sa + (cur * BM + wm * (FM * 16) + (l & 15)) * LDK + 8 * (l >> 4);
     const bf16* cb = sb + (cur * BN + wn * 64 + (l & 15)) * LDK + 8 * (l >> 4);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 a[4], b[4];
+      // B fragments, then the A fragments one ahead of their 4 MFMAs (all
+      // of them at once spills at 8 x 4 accumulators)
+      bf16x8 bv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ca + 16 * i * LDK + 32 * ks);
+      for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const bf16x8*>(cb + 16 * j * LDK + 32 * ks);
+      bf16x8 av = *reinterpret_cast<const bf16x8*>(ca + 32 * ks);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(cb + 16 * j * LDK + 32 * ks);
+      for (int i = 0; i < FM; ++i) {
+        bf16x8 an = av;
+        if (i + 1 < FM) an = *reinterpret_cast<const bf16x8*>(ca + 16 * (i + 1) * LDK + 32 * ks);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+#ifdef FBERT_AB_NOMFMA  // A/B probe only: the data movement alone
+          acc[i][j][0] += (float)av[j] * (float)bv[j][i & 7];
+#else
+          // W as the A operand: D = W_j . A_i^T, so a lane's four outputs are
+          // four consecutive columns of one row (8 / 16-byte stores)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av, acc[i][j], 0, 0, 0);
+#endif
+        }
+        av = an;
+      }
     }
     // the other buffer was last read before the previous barrier
     if (kt + 1 < KT) store_lds(cur ^ 1);
     __syncthreads();
   }
-  // C/D of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg
+#ifdef FBERT_AB_NOEPI  // A/B probe only (tools/gemm_probe.hip): the main loop alone
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  if (sum == 12345.678f) reinterpret_cast<float*>(out)[tid] = sum;
+  return;
+#endif
+  // D of 16x16x32 with W as A: row = lane & 15, col = 4 (lane >> 4) + reg
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + 16 * j + (l & 15);
+    const int col = n0 + wn * 64 + 16 * j + 4 * (l >> 4);
     if (col >= N) continue;
-    const float bv = bias[col];
+    const float4 bv4 = *reinterpret_cast<const float4*>(bias + col);  // N % 4 == 0 (fhe_bert_create)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i) {
+      const int row = m0 + wm * (FM * 16) + 16 * i + (l & 15);
+      if (row >= M) continue;
+      float v[4] = {acc[i][j][0] + bv4.x, acc[i][j][1] + bv4.y, acc[i][j][2] + bv4.z, acc[i][j][3] + bv4.w};
+      const size_t o = (size_t)row * N + col;
+      if constexpr (EPI == EPI_RESID_F32) {
+        const float4 rs = *reinterpret_cast<const float4*>(resid + o);
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) =
+            make_float4(v[0] + rs.x, v[1] + rs.y, v[2] + rs.z, v[3] + rs.w);
+      } else {
+        if constexpr (EPI == EPI_GELU_BF16) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + 16 * i + 4 * (l >> 4) + r;
-        if (row >= M) continue;
-        float v = acc[i][j][r] + bv;
-        const size_t o = (size_t)row * N + col;
-        if constexpr (EPI == EPI_RESID_F32) {
-          reinterpret_cast<float*>(out)[o] = v + resid[o];
-        } else {
-          if constexpr (EPI == EPI_GELU_BF16) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-          reinterpret_cast<bf16*>(out)[o] = (bf16)v;
+          for (int rr = 0; rr < 4; ++rr) v[rr] = 0.5f * v[rr] * (1.0f + erff(v[rr] * 0.70710678118654752f));
         }
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(out) + o) = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       }
+    }
   }
 }
 
@@ -552,18 +602,33 @@ int fhe_bert_profile_read(fhe_bert* h, const char* kernel, double* total_ms, int
   return FHE_OK;
 }
 
+template <int EPI, int BN>
+static void gemm_launch(const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M, int N,
+                        int K, hipStream_t st) {
+  const int tiles_n = (N + BN - 1) / BN, nblk = tiles_n * ((M + BM - 1) / BM);
+  hipLaunchKernelGGL((k_gemm<EPI, BN>), dim3((unsigned)nblk), dim3(512), gemm_lds<BN>(), st, A, W, bias, resid, out, M,
+                     N, K, tiles_n, nblk);
+}
+
 template <int EPI>
 static int gemm(fhe_bert* h, const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M,
                 int N, int K, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    BCHK(h, hipFuncSetAttribute((const void*)k_gemm<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, GEMM_LDS));
+    BCHK(h, hipFuncSetAttribute((const void*)k_gemm<EPI, 256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                gemm_lds<256>()));
+    BCHK(h, hipFuncSetAttribute((const void*)k_gemm<EPI, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                gemm_lds<128>()));
     attr = true;
   }
   hipEvent_t e1;
   pbegin(h, h->p_gemm, st, &e1);
-  hipLaunchKernelGGL(k_gemm<EPI>, dim3((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM)), dim3(256),
-                     GEMM_LDS, st, A, W, bias, resid, out, M, N, K);
+  // 256-wide tiles unless that leaves fewer than ~2 tiles per CU (N = 768 at
+  // 25.6k tokens: 300 tiles against 600 at 128)
+  if ((int64_t)((N + 255) / 256) * ((M + BM - 1) / BM) >= 512)
+    gemm_launch<EPI, 256>(A, W, bias, resid, out, M, N, K, st);
+  else
+    gemm_launch<EPI, 128>(A, W, bias, resid, out, M, N, K, st);
   pend(h, h->p_gemm, st, e1, 2.0 * M * N * K);
   BCHK(h, hipGetLastError());
   return FHE_OK;
