@@ -204,8 +204,16 @@ __global__ void __launch_bounds__(256) k_keyswitch_mfma(const v4i* __restrict__ 
                                                         int KB, u64* __restrict__ out) {
   __shared__ v4i bt[2][8 * 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nb = blockIdx.y;
-  const int64_t cb = (int64_t)blockIdx.x * 4 + w;
+  // XCD-aware order over the (ciphertext group, column block) grid: block b
+  // runs on XCD b % 8, and each XCD takes a contiguous run of column blocks
+  // with all their ciphertext groups, so a column block's key tiles come
+  // into one XCD's L2 once for every group (the groups of one column block
+  // dispatched round-robin over the XCDs made each XCD stream the whole key)
+  const int nblk = (int)gridDim.x, bid = (int)blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ngrp = nblk / NB;
+  const int nb = t / ngrp;
+  const int64_t cb = (int64_t)(t - nb * ngrp) * 4 + w;
   const bool act = cb * 16 < count;
   const v4i zero = {0, 0, 0, 0};
   const v4i* Dv = D + (size_t)cb * KB * 64 + lane;
