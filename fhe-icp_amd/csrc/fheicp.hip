@@ -897,7 +897,7 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
     ctx->prof_ks.kernel = "k_keyswitch_mfma";
     hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)(p.k * p.N / 64), (unsigned)ncb), dim3(256), 0, st, d_big, count,
                        p.k * p.N, p.ks_base_log, p.ks_level, shift, add_body, KB, D, body);
-    hipLaunchKernelGGL(k_keyswitch_mfma, dim3((unsigned)(((count + 63) / 64) * NB)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_keyswitch_mfma, dim3((unsigned)(((count + KSM_CTS - 1) / KSM_CTS) * NB)), dim3(256), 0, st,
                        (const v4i*)D, (const v4i*)ctx->ksk8, body, count, n1, NB, KB, d_small);
     prof_end(ctx, ctx->prof_ks, st, e1, count);
     HIPCHK(ctx, hipGetLastError());

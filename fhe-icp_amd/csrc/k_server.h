@@ -197,64 +197,95 @@ __global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, i
   }
 }
 
-// workgroup = 4 waves = 64 ciphertexts x 16 columns x 8 byte planes; the key
-// tile of each k-block (8 KB) is shared through double-buffered LDS
+// workgroup = 4 waves = 128 ciphertexts x 16 columns x 8 byte planes: each
+// wave two 16-ciphertext groups, so every key fragment read from LDS feeds two
+// MFMAs (one per group: with one, the four waves' fragment reads, 1 KB per
+// MFMA, saturate the LDS). The key tile of each k-block (8 KB) is shared
+// through LDS; the tiles and the digit fragments stream through a register
+// ring 4 k-blocks deep (the loads of k-block k + 4 are issued at k-block k;
+// the compiler counts their vmcnt), and the tiles pass through 3 LDS buffers
+// with one barrier per k-block: the tile of k + 1 is written while the
+// slowest wave may still read k - 1. KB % 4 == 0 for every supported
+// parameter set (kN / 64 is a multiple of 4).
+constexpr int KSM_RING = 4, KSM_CTS = 128;  // ciphertexts per workgroup
 __global__ void __launch_bounds__(256) k_keyswitch_mfma(const v4i* __restrict__ D, const v4i* __restrict__ K8,
                                                         const u64* __restrict__ body, int64_t count, int n1, int NB,
                                                         int KB, u64* __restrict__ out) {
-  __shared__ v4i bt[2][8 * 64];
+  __shared__ v4i bt[3][8 * 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // XCD-aware order over the (ciphertext group, column block) grid: block b
+  // XCD-aware order over the (ciphertext block, column block) grid: block b
   // runs on XCD b % 8, and each XCD takes a contiguous run of column blocks
-  // with all their ciphertext groups, so a column block's key tiles come
-  // into one XCD's L2 once for every group (the groups of one column block
+  // with all their ciphertext blocks, so a column block's key tiles come
+  // into one XCD's L2 once for every block (the blocks of one column block
   // dispatched round-robin over the XCDs made each XCD stream the whole key)
   const int nblk = (int)gridDim.x, bid = (int)blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int ngrp = nblk / NB;
   const int nb = t / ngrp;
-  const int64_t cb = (int64_t)(t - nb * ngrp) * 4 + w;
-  const bool act = cb * 16 < count;
-  const v4i zero = {0, 0, 0, 0};
-  const v4i* Dv = D + (size_t)cb * KB * 64 + lane;
+  const int64_t ncb = (count + 15) / 16;                         // 16-ciphertext groups (digit rows)
+  const int64_t cb0 = (int64_t)(t - nb * ngrp) * (KSM_CTS / 16) + 2 * w;
+  // a group past the batch streams group 0's digits and stores nothing
+  const v4i* Dv0 = D + (size_t)(cb0 < ncb ? cb0 : 0) * KB * 64 + lane;
+  const v4i* Dv1 = D + (size_t)(cb0 + 1 < ncb ? cb0 + 1 : 0) * KB * 64 + lane;
   const v4i* Kv = K8 + (size_t)nb * 8 * 64;
-  v4i acc[8];
+  const size_t kstride = (size_t)NB * 8 * 64;  // v4i per k-block of the key
+  v4i acc[2][8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = zero;
-  bt[0][tid] = Kv[tid];
-  bt[0][tid + 256] = Kv[tid + 256];
-  v4i a = act ? Dv[0] : zero;
-  __syncthreads();
-  for (int kb = 0; kb < KB; ++kb) {
-    const int cur = kb & 1;
-    v4i n0 = zero, n1v = zero, an = zero;
-    const bool more = kb + 1 < KB;
-    if (more) {
-      const v4i* srcp = Kv + (size_t)(kb + 1) * NB * 8 * 64;
-      n0 = srcp[tid];
-      n1v = srcp[tid + 256];
-      if (act) an = Dv[(size_t)(kb + 1) * 64];
-    }
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bt[cur][q * 64 + lane], acc[q], 0, 0, 0);
-    if (more) {
-      bt[cur ^ 1][tid] = n0;
-      bt[cur ^ 1][tid + 256] = n1v;
-      a = an;
-    }
-    __syncthreads();
+    for (int q = 0; q < 8; ++q) acc[h][q] = (v4i){0, 0, 0, 0};
+  v4i rk[KSM_RING][2], rd[KSM_RING][2];
+  // prologue: k-blocks 0..3 in flight, k-block 0's tile into LDS
+#pragma unroll
+  for (int j = 0; j < KSM_RING; ++j) {
+    rk[j][0] = Kv[j * kstride + tid];
+    rk[j][1] = Kv[j * kstride + tid + 256];
+    rd[j][0] = Dv0[(size_t)j * 64];
+    rd[j][1] = Dv1[(size_t)j * 64];
   }
-  if (!act) return;
+  bt[0][tid] = rk[0][0];
+  bt[0][tid + 256] = rk[0][1];
+  for (int kb = 0; kb < KB; kb += KSM_RING) {
+#pragma unroll
+    for (int j = 0; j < KSM_RING; ++j) {
+      const int k = kb + j;
+      // ring slot j held k-block k, written to LDS at k - 1 (or the prologue):
+      // reuse it for k + 4 (clamped at the end: reloads, no branch)
+      const int kn = min(k + KSM_RING, KB - 1);
+      rk[j][0] = Kv[kn * kstride + tid];
+      rk[j][1] = Kv[kn * kstride + tid + 256];
+      // k-block k + 1's tile (loaded 3 k-blocks ago) into its LDS buffer
+      const int j1 = (j + 1) % KSM_RING;
+      if (k + 1 < KB) {
+        bt[(k + 1) % 3][tid] = rk[j1][0];
+        bt[(k + 1) % 3][tid + 256] = rk[j1][1];
+      }
+      __syncthreads();
+      const v4i a0 = rd[j][0], a1 = rd[j][1];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const v4i bq = bt[k % 3][q * 64 + lane];
+        acc[0][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq, acc[0][q], 0, 0, 0);
+        acc[1][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq, acc[1][q], 0, 0, 0);
+      }
+      rd[j][0] = Dv0[(size_t)kn * 64];
+      rd[j][1] = Dv1[(size_t)kn * 64];
+    }
+  }
   const int col = nb * KSM_NB_COLS + (lane & 15);
   if (col >= n1) return;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t c = cb * 16 + 4 * (lane >> 4) + r;
-    if (c >= count) continue;
-    u64 v = 0;
+  for (int h = 0; h < 2; ++h) {
+    if (cb0 + h >= ncb) continue;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v += (u64)(int64_t)acc[q][r] << (8 * q);
-    out[(size_t)c * n1 + col] = (col == n1 - 1 ? body[c] : (u64)0) - v;
+    for (int r = 0; r < 4; ++r) {
+      const int64_t c = (cb0 + h) * 16 + 4 * (lane >> 4) + r;
+      if (c >= count) continue;
+      u64 v = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v += (u64)(int64_t)acc[h][q][r] << (8 * q);
+      out[(size_t)c * n1 + col] = (col == n1 - 1 ? body[c] : (u64)0) - v;
+    }
   }
 }
 
