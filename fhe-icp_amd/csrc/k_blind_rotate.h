@@ -1033,6 +1033,9 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb64(const 
 }
 
 // ---- classic blind rotation with key-stationary products ---------------------
+#ifndef FHEICP_V4S_PARK
+#define FHEICP_V4S_PARK 5
+#endif
 // k_blind_rotate_v4's step (rotation through the own slot, digits, L forward
 // transforms, one inverse per wave) with the product phase of
 // k_blind_rotate_mb: wave (g, c) forms output component c of all four
@@ -1054,6 +1057,12 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
   __shared__ c64 xbuf[G * WPC * SCR];
   __shared__ c64 twl[NTW];
   __shared__ uint16_t atab[G][NMAX + 1];
+  // 64-bit accumulators from L = 4: PARK of the 16 words per lane wait out the
+  // step in LDS (written after the rotation has read them, read back for the
+  // update), 10 VGPRs less over the level loop, which otherwise spilled 56 B
+  // per step to scratch (FHEICP_V4S_PARK = 0: A/B builds)
+  constexpr int PARK = (!A32 && L >= 4) ? FHEICP_V4S_PARK : 0;
+  __shared__ u64 park[PARK > 0 ? PARK * G * WPC * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = w / WPC, comp = w - g * WPC;
@@ -1155,6 +1164,10 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
         for (int l = 1; l < L; ++l) dg[l - 1][s] = (uint32_t)(d[0][l] & 0xffff) | ((uint32_t)d[1][l] << 16);
       }
     }
+    if constexpr (PARK > 0) {
+#pragma unroll
+      for (int s = 0; s < PARK; ++s) park[(s * G * WPC + w) * 64 + lane] = acc[s];
+    }
     V4_STAMP(1);
     if constexpr (br_prio_fine<L>()) V4S_PRIO(1);
     c64 o[G][2];
@@ -1218,6 +1231,10 @@ __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_v4s(const u
 #pragma unroll
     for (int u = 0; u < S; ++u) ov[u] = slot[u * 64 + lane];
     inverse(ov, twl, slot, lane);
+    if constexpr (PARK > 0) {
+#pragma unroll
+      for (int s = 0; s < PARK; ++s) acc[s] = park[(s * G * WPC + w) * 64 + lane];
+    }
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       acc[u] += AT::from_f64(ov[u].x);
