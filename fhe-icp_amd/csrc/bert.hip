@@ -27,66 +27,63 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---- GEMM: out[M][N] = A[M][K] . W[N][K]^T + bias (+ epilogue) ------------
-// 256 x BN block tile (BN = 256, or 128 when N is small: more tiles than
-// CUs), K step 64, 8 waves of 512 threads in (8 / (BN/64)) x (BN/64), each a
-// (256 / waves_m) x 64 tile of 16 x 16 v_mfma_f32_16x16x32_bf16 accumulators
-// (8 x 4 at BN = 256: 0.375 LDS fragment reads per MFMA). Operands go
-// global -> registers -> LDS, double buffered: the next K step's loads are in
-// flight during this step's 64 MFMAs per wave, one barrier per K step. LDS
-// rows are padded to 72 bf16 (144 B = 9 x 16 B), so the 16 lanes of a
-// ds_read_b128 group (rows l & 15) land on 16 distinct bank quads (9 r mod 16
-// is a permutation). Tiles are numbered row-major and dealt XCD by XCD, so
-// the column tiles of one 256-row band (which share its A rows) run on one
-// XCD's L2.
-constexpr int BM = 256, BK = 64, LDK = BK + 8;
-template <int BN>
-constexpr int gemm_lds() { return 2 * (BM + BN) * LDK * (int)sizeof(bf16); }  // 147456 / 110592 B
+// Shared pieces of the GEMM below: the 256-row block tile and K step, the
+// epilogues, and the erf of BERT's GELU.
+constexpr int BM = 256, BK = 64;
 enum { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2 };
 
-template <int EPI, int BN>
-__global__ void __launch_bounds__(512) k_gemm(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                              const float* __restrict__ bias, const float* __restrict__ resid,
-                                              void* __restrict__ out, int M, int N, int K, int tiles_n, int nblk) {
-  constexpr int WN = BN / 64, WM = 8 / WN;  // waves along N and M
-  constexpr int FM = BM / WM / 16;          // 16-row fragments per wave
-  constexpr int AL = BM * BK / 8 / 512, BL = BN * BK / 8 / 512;  // 16-byte loads per thread
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
+// rounding of the GELU output): one reciprocal, one exp and five FMAs against
+// the library erff's ~3x the instructions, which made the FFN GEMM's epilogue
+// as long as its main loop
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+  const float p = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
+                       0.254829592f) * t;
+  return copysignf(1.0f - p * __expf(-ax * ax), x);
+}
+
+// ---- GEMM, LDS-DMA form: 256 x 128 tiles, three stages -------------------
+// The operands go global -> LDS directly (global_load_lds_dwordx4, no staging
+// registers) into three stage buffers, so the loads of K step kt + 2 are in
+// flight while step kt computes. An LDS-DMA instruction writes 64 lanes x 16
+// bytes contiguously, so the rows are unpadded (128 B) and the bank spread
+// comes from an XOR swizzle applied on the global side: LDS chunk c' of row r
+// holds the row's chunk c' ^ (r & 7). Waits are counted by hand (vmcnt(6):
+// one stage of six loads per wave left in flight) before a raw s_barrier.
+constexpr int G3_BN = 128, G3_STAGE = (BM + G3_BN) * BK;  // bf16 elements per stage (48 KB)
+constexpr int G3_LDS = 3 * G3_STAGE * (int)sizeof(bf16);   // 147456 B
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int EPI>
+__global__ void __launch_bounds__(512) k_gemm3(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                               const float* __restrict__ bias, const float* __restrict__ resid,
+                                               void* __restrict__ out, int M, int N, int K, int tiles_n, int nblk) {
+  constexpr int BN = G3_BN, WN = 2, FM = 4;  // 8 waves in 4 x 2, each 64 x 64
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* sa = reinterpret_cast<bf16*>(smem);   // [2][BM][LDK]
-  bf16* sb = sa + 2 * BM * LDK;               // [2][BN][LDK]
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  bf16* st = reinterpret_cast<bf16*>(smem);
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w / WN, wn = w - wm * WN;
-  // XCD-aware tile order (bijective for any nblk): block b runs on XCD b % 8
   const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
   const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
   const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * BN;
   const int KT = K / BK;
-  uint4 ra[AL], rb[BL];
-  auto load_regs = [&](int kt) {
+  auto issue = [&](int kt, int s) {
+    bf16* la = st + s * G3_STAGE;
+    bf16* lb = la + BM * BK;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
-      // (guarded loads: unguarded ones from a clamped row let the scheduler
-      // hoist every fragment read and spill the staging registers)
-      const int gm = m0 + row;
-      ra[i] = gm < M ? *reinterpret_cast<const uint4*>(A + (size_t)gm * K + kt * BK + kc) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {  // A: 32 pieces of 8 rows x 128 B, four per wave
+      const int pc = 4 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+      const int gm = min(m0 + row, M - 1);  // rows past M: loaded, never stored
+      __builtin_amdgcn_global_load_lds(A + (size_t)gm * K + kt * BK + 8 * c, (lds_void*)(la + pc * 8 * BK), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
-      const int gn = n0 + row;
-      rb[i] = gn < N ? *reinterpret_cast<const uint4*>(W + (size_t)gn * K + kt * BK + kc) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store_lds = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
-      *reinterpret_cast<uint4*>(sa + (buf * BM + row) * LDK + kc) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int c = tid + 512 * i, row = c >> 3, kc = (c & 7) * 8;
-      *reinterpret_cast<uint4*>(sb + (buf * BN + row) * LDK + kc) = rb[i];
+    for (int i = 0; i < 2; ++i) {  // B: 16 pieces, two per wave
+      const int pc = 2 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+      const int gn = min(n0 + row, N - 1);
+      __builtin_amdgcn_global_load_lds(W + (size_t)gn * K + kt * BK + 8 * c, (lds_void*)(lb + pc * 8 * BK), 16, 0, 0);
     }
   };
   f32x4 acc[FM][4];
@@ -94,45 +91,37 @@ __global__ void __launch_bounds__(512) k_gemm(const bf16* __restrict__ A, const 
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  load_regs(0);
-  store_lds(0);
-  __syncthreads();
+  issue(0, 0);
+  if (KT > 1) issue(1, 1);
   for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_regs(kt + 1);  // in flight during the MFMAs
-    const bf16* ca = sa + (cur * BM + wm * (FM * 16) + (l & 15)) * LDK + 8 * (l >> 4);
-    const bf16* cb = sb + (cur * BN + wn * 64 + (l & 15)) * LDK + 8 * (l >> 4);
+    if (kt + 1 < KT)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < KT) issue(kt + 2, (kt + 2) % 3);
+    const bf16* la = st + (kt % 3) * G3_STAGE;
+    const bf16* lb = la + BM * BK;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      // B fragments, then the A fragments one ahead of their 4 MFMAs (all
-      // of them at once spills at 8 x 4 accumulators)
+      const int c = 4 * ks + (l >> 4);
       bf16x8 bv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const bf16x8*>(cb + 16 * j * LDK + 32 * ks);
-      bf16x8 av = *reinterpret_cast<const bf16x8*>(ca + 32 * ks);
+      for (int j = 0; j < 4; ++j) {
+        const int n = wn * 64 + 16 * j + (l & 15);
+        bv[j] = *reinterpret_cast<const bf16x8*>(lb + n * BK + 8 * (c ^ (n & 7)));
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        bf16x8 an = av;
-        if (i + 1 < FM) an = *reinterpret_cast<const bf16x8*>(ca + 16 * (i + 1) * LDK + 32 * ks);
+        const int m = wm * (FM * 16) + 16 * i + (l & 15);
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(la + m * BK + 8 * (c ^ (m & 7)));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#ifdef FBERT_AB_NOMFMA  // A/B probe only: the data movement alone
-          acc[i][j][0] += (float)av[j] * (float)bv[j][i & 7];
-#else
-          // W as the A operand: D = W_j . A_i^T, so a lane's four outputs are
-          // four consecutive columns of one row (8 / 16-byte stores)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av, acc[i][j], 0, 0, 0);
-#endif
-        }
-        av = an;
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv[j], av, acc[i][j], 0, 0, 0);
       }
     }
-    // the other buffer was last read before the previous barrier
-    if (kt + 1 < KT) store_lds(cur ^ 1);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's reads retire before the next barrier
   }
-#ifdef FBERT_AB_NOEPI  // A/B probe only (tools/gemm_probe.hip): the main loop alone
+#ifdef FBERT_AB_NOEPI
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -141,32 +130,62 @@ __global__ void __launch_bounds__(512) k_gemm(const bf16* __restrict__ A, const 
   if (sum == 12345.678f) reinterpret_cast<float*>(out)[tid] = sum;
   return;
 #endif
-  // D of 16x16x32 with W as A: row = lane & 15, col = 4 (lane >> 4) + reg
+  // Epilogue through LDS: each wave writes its 64 x 64 tile (bias added, GELU
+  // applied) row-major into a private region, then stores whole 128-byte row
+  // pieces, 16 bytes per lane (written straight from the fragments, a lane's
+  // four columns made 32-byte row pieces and the FFN GEMM's epilogue ran at
+  // 1.4 TB/s). Rows are padded by 16 bytes against bank conflicts.
+  __syncthreads();  // every wave is done with the stage buffers
+  const int colw = n0 + wn * 64, roww = m0 + wm * 64;
+  if (colw >= N) return;  // N % 64 == 0: a wave's columns are all in or all out
+  constexpr bool F32 = EPI == EPI_RESID_F32;
+  constexpr int EPL = F32 ? 68 : 72;  // row pitch in elements (272 / 144 bytes)
+  char* ep = smem + (size_t)w * (64 * 68 * 4);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + 16 * j + 4 * (l >> 4);
-    if (col >= N) continue;
-    const float4 bv4 = *reinterpret_cast<const float4*>(bias + col);  // N % 4 == 0 (fhe_bert_create)
+    const int c = 16 * j + 4 * (l >> 4);
+    const float4 bv4 = *reinterpret_cast<const float4*>(bias + colw + c);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int row = m0 + wm * (FM * 16) + 16 * i + (l & 15);
-      if (row >= M) continue;
+      const int rl = 16 * i + (l & 15);
       float v[4] = {acc[i][j][0] + bv4.x, acc[i][j][1] + bv4.y, acc[i][j][2] + bv4.z, acc[i][j][3] + bv4.w};
-      const size_t o = (size_t)row * N + col;
-      if constexpr (EPI == EPI_RESID_F32) {
-        const float4 rs = *reinterpret_cast<const float4*>(resid + o);
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) =
-            make_float4(v[0] + rs.x, v[1] + rs.y, v[2] + rs.z, v[3] + rs.w);
+      if constexpr (F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep) + rl * EPL + c) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         if constexpr (EPI == EPI_GELU_BF16) {
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) v[rr] = 0.5f * v[rr] * (1.0f + erff(v[rr] * 0.70710678118654752f));
+          for (int rr = 0; rr < 4; ++rr) v[rr] = 0.5f * v[rr] * (1.0f + erf_fast(v[rr] * 0.70710678118654752f));
         }
         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(out) + o) = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(ep) + rl * EPL + c) =
+            (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       }
     }
   }
+  constexpr int CPR = F32 ? 16 : 8;  // 16-byte pieces per 64-column row
+#pragma unroll
+  for (int it = 0; it < 64 * CPR / 64; ++it) {
+    const int pc = l + 64 * it, rl = pc / CPR, cp = pc - rl * CPR;
+    const int row = roww + rl;
+    if (row >= M) continue;
+    if constexpr (F32) {
+      const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ep) + rl * EPL + 4 * cp);
+      const size_t o = (size_t)row * N + colw + 4 * cp;
+      const float4 rs = *reinterpret_cast<const float4*>(resid + o);
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = make_float4(v.x + rs.x, v.y + rs.y, v.z + rs.z, v.w + rs.w);
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(ep) + rl * EPL + 8 * cp);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(out) + (size_t)row * N + colw + 8 * cp) = v;
+    }
+  }
+}
+
+template <int EPI>
+static void gemm3_launch(const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M, int N,
+                         int K, hipStream_t st) {
+  const int tiles_n = (N + G3_BN - 1) / G3_BN, nblk = tiles_n * ((M + BM - 1) / BM);
+  hipLaunchKernelGGL(k_gemm3<EPI>, dim3((unsigned)nblk), dim3(512), G3_LDS, st, A, W, bias, resid, out, M, N, K,
+                     tiles_n, nblk);
 }
 
 // ---- fused attention (flash-style) ------------------------------------------
@@ -602,33 +621,19 @@ int fhe_bert_profile_read(fhe_bert* h, const char* kernel, double* total_ms, int
   return FHE_OK;
 }
 
-template <int EPI, int BN>
-static void gemm_launch(const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M, int N,
-                        int K, hipStream_t st) {
-  const int tiles_n = (N + BN - 1) / BN, nblk = tiles_n * ((M + BM - 1) / BM);
-  hipLaunchKernelGGL((k_gemm<EPI, BN>), dim3((unsigned)nblk), dim3(512), gemm_lds<BN>(), st, A, W, bias, resid, out, M,
-                     N, K, tiles_n, nblk);
-}
-
 template <int EPI>
 static int gemm(fhe_bert* h, const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M,
                 int N, int K, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    BCHK(h, hipFuncSetAttribute((const void*)k_gemm<EPI, 256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                gemm_lds<256>()));
-    BCHK(h, hipFuncSetAttribute((const void*)k_gemm<EPI, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                gemm_lds<128>()));
+    BCHK(h, hipFuncSetAttribute((const void*)k_gemm3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS));
     attr = true;
   }
   hipEvent_t e1;
   pbegin(h, h->p_gemm, st, &e1);
-  // 256-wide tiles unless that leaves fewer than ~2 tiles per CU (N = 768 at
-  // 25.6k tokens: 300 tiles against 600 at 128)
-  if ((int64_t)((N + 255) / 256) * ((M + BM - 1) / BM) >= 512)
-    gemm_launch<EPI, 256>(A, W, bias, resid, out, M, N, K, st);
-  else
-    gemm_launch<EPI, 128>(A, W, bias, resid, out, M, N, K, st);
+  // the three-stage LDS-DMA form everywhere (tools/gemm_probe.hip against the
+  // register-staged k_gemm: 12-34% faster on the four BERT shapes)
+  gemm3_launch<EPI>(A, W, bias, resid, out, M, N, K, st);
   pend(h, h->p_gemm, st, e1, 2.0 * M * N * K);
   BCHK(h, hipGetLastError());
   return FHE_OK;

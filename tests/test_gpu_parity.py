@@ -88,6 +88,23 @@ def test_linear_and_keyswitch_bit_exact(which, request):
         assert np.array_equal(u64(ks), ks_ref), f"keyswitch shift={shift}"
 
 
+@pytest.mark.parametrize("B", [1, 17, 300])
+def test_keyswitch_ragged_batches_bit_exact(real, B):
+    """The MFMA key switch (k_keyswitch_mfma: 128 ciphertexts per workgroup,
+    two 16-ciphertext groups per wave, a 4-deep load ring) on batches that
+    leave idle waves and half-empty groups: bit-exact against the oracle."""
+    eng, ref = real
+    P = eng.msg_bits
+    rng = np.random.default_rng(60 + B)
+    v = rng.integers(-(2 ** (P - 1)), 2 ** (P - 1), B)
+    ct = eng.encrypt(v, seed=61, id0=7 * B)
+    ct_ref = ref.encrypt_ints(v, seed=61, id0=7 * B)
+    ks = eng.keyswitch(ct, 2, 1 << 61)
+    sh = ct_ref << np.uint64(2)
+    sh[:, -1] += np.uint64(1 << 61)
+    assert np.array_equal(u64(ks), ref.keyswitch(sh))
+
+
 def test_pbs_matches_oracle_toy(toy):
     eng, ref = toy
     rng = np.random.default_rng(7)

@@ -1,10 +1,11 @@
-// A/B probe of the BERT GEMM (fhe-icp_amd/csrc/bert.hip k_gemm) at the embed
-// bench's shapes (25.6k tokens): HIP-event time per launch and TFLOP/s.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DFBERT_AB_NOEPI|-DFBERT_AB_NOMFMA]
+// Probe of the BERT GEMM (fhe-icp_amd/csrc/bert.hip k_gemm3) at the embed
+// bench's shapes (25.6k tokens, random bf16 operands): HIP-event time per
+// launch and TFLOP/s. Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DFBERT_AB_NOEPI]
 //        tools/gemm_probe.hip -o gemm_probe
 #include "../fhe-icp_amd/csrc/bert.hip"
 
 #include <cstdio>
+#include <vector>
 
 int main() {
   using namespace fbert;
@@ -18,22 +19,30 @@ int main() {
   hipMalloc(&bias, 3072 * 4);
   hipMalloc(&resid, (size_t)M * 3072 * 4);
   hipMalloc(&out, (size_t)M * 3072 * 4);
-  hipMemset(A, 0x3c, (size_t)M * 3072 * 2);  // bf16 ~1.1: finite, nonzero
-  hipMemset(W, 0x3c, (size_t)3072 * 3072 * 2);
+  {  // random bf16 in [-1, 1): exponent 0x3f00-0x3f7f (0.5-1) with random sign and mantissa
+    std::vector<uint16_t> h((size_t)M * 3072);
+    uint32_t x = 12345;
+    for (auto& v : h) {
+      x = x * 1664525u + 1013904223u;
+      v = (uint16_t)(0x3e80 + ((x >> 9) & 0x7f) + (((x >> 20) & 1) << 15) + (((x >> 21) & 1) << 7));
+    }
+    hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    hipMemcpy(W, h.data(), (size_t)3072 * 3072 * 2, hipMemcpyHostToDevice);
+  }
   hipMemset(bias, 0, 3072 * 4);
   hipMemset(resid, 0, (size_t)M * 3072 * 4);
-  hipFuncSetAttribute((const void*)k_gemm<0, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, gemm_lds<256>());
-  hipFuncSetAttribute((const void*)k_gemm<1, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, gemm_lds<256>());
-  hipFuncSetAttribute((const void*)k_gemm<2, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, gemm_lds<128>());
+  hipFuncSetAttribute((const void*)k_gemm3<0>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
+  hipFuncSetAttribute((const void*)k_gemm3<1>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
+  hipFuncSetAttribute((const void*)k_gemm3<2>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   for (auto& sh : shapes) {
     const int N = sh[0], K = sh[1], epi = sh[2];
     auto run = [&]() {
-      if (epi == 0) gemm_launch<0, 256>(A, W, bias, resid, out, M, N, K, 0);
-      else if (epi == 1) gemm_launch<1, 256>(A, W, bias, resid, out, M, N, K, 0);
-      else gemm_launch<2, 128>(A, W, bias, resid, out, M, N, K, 0);
+      if (epi == 0) gemm3_launch<0>(A, W, bias, resid, out, M, N, K, 0);
+      else if (epi == 1) gemm3_launch<1>(A, W, bias, resid, out, M, N, K, 0);
+      else gemm3_launch<2>(A, W, bias, resid, out, M, N, K, 0);
     };
     run();
     hipEventRecord(e0, 0);
