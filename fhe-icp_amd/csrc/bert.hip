@@ -354,6 +354,45 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
   ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb + (size_t)row * H, H);
 }
 
+// the same LayerNorm with 16-byte accesses (H % 256 == 0): lane l holds
+// columns 4l..4l+3 of each 256-column piece, so a row of 768 is three
+// float4 loads per lane instead of twelve dword loads
+__global__ void __launch_bounds__(256) k_layernorm4(const float* __restrict__ x, const float* __restrict__ g,
+                                                    const float* __restrict__ be, float* __restrict__ y,
+                                                    bf16* __restrict__ yb, int M, int H, float eps) {
+  const int l = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nv = H / 256;  // <= LN_MAXV / 4
+  float4 v[LN_MAXV / 4];
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < LN_MAXV / 4; ++j) {
+    if (j >= nv) break;
+    v[j] = *reinterpret_cast<const float4*>(x + (size_t)row * H + j * 256 + 4 * l);
+    s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  }
+  const float mean = wave_sum(s) / (float)H;
+  float q = 0.0f;
+#pragma unroll
+  for (int j = 0; j < LN_MAXV / 4; ++j) {
+    if (j >= nv) break;
+    const float a = v[j].x - mean, b = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+    q += (a * a + b * b) + (c * c + d * d);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)H + eps);
+#pragma unroll
+  for (int j = 0; j < LN_MAXV / 4; ++j) {
+    if (j >= nv) break;
+    const int c = j * 256 + 4 * l;
+    const float4 gg = *reinterpret_cast<const float4*>(g + c), bb = *reinterpret_cast<const float4*>(be + c);
+    const float4 r = make_float4((v[j].x - mean) * rstd * gg.x + bb.x, (v[j].y - mean) * rstd * gg.y + bb.y,
+                                 (v[j].z - mean) * rstd * gg.z + bb.z, (v[j].w - mean) * rstd * gg.w + bb.w);
+    *reinterpret_cast<float4*>(y + (size_t)row * H + c) = r;
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<bf16x4*>(yb + (size_t)row * H + c) = (bf16x4){(bf16)r.x, (bf16)r.y, (bf16)r.z, (bf16)r.w};
+  }
+}
+
 __global__ void __launch_bounds__(256) k_embed_ln(const int32_t* __restrict__ ids, const int32_t* __restrict__ tt,
                                                   const float* __restrict__ we, const float* __restrict__ pe,
                                                   const float* __restrict__ te, const float* __restrict__ g,
@@ -698,12 +737,18 @@ int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, c
     BCHK(h, hipGetLastError());
     if ((rc = gemm<EPI_RESID_F32>(h, ctx, L.wo, L.bo, hs, tmp, M, H, H, st))) return rc;
     pbegin(h, h->p_other, st, &e1);
-    hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps);
+    if (H % 256 == 0)
+      hipLaunchKernelGGL(k_layernorm4, dim3(rows4), dim3(256), 0, st, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps);
+    else
+      hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps);
     pend(h, h->p_other, st, e1, 0.0);
     if ((rc = gemm<EPI_GELU_BF16>(h, hb, L.wi, L.bi, nullptr, inter, M, I, H, st))) return rc;
     if ((rc = gemm<EPI_RESID_F32>(h, inter, L.wo2, L.bo2, hs, tmp, M, H, I, st))) return rc;
     pbegin(h, h->p_other, st, &e1);
-    hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps);
+    if (H % 256 == 0)
+      hipLaunchKernelGGL(k_layernorm4, dim3(rows4), dim3(256), 0, st, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps);
+    else
+      hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps);
     pend(h, h->p_other, st, e1, 0.0);
     BCHK(h, hipGetLastError());
   }
