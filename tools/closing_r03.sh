@@ -7,7 +7,7 @@
 # stage, the SQ counters of the headline and C5 kernels, and a 2-rank gloo
 # rehearsal of the N > 1 (C4, 100k docs) path.
 set -u -o pipefail
-T=${1:-r03m}
+T=${1:-r03s}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"; cd "$R"
 step() { echo "== $1 $(date +%T)" >> "$OUT/${T}_steps.log"; }
 step tests; timeout -k 10 900 python -u -m pytest tests/ -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/${T}_tests.log" 2>&1 || exit 1
