@@ -176,3 +176,30 @@ def test_bert_abi_validation():
         assert L.fhe_bert_create(C.byref(BertConfigC(**bad)), 0, C.byref(h)) == -1, bad
     assert L.fhe_bert_create(C.byref(BertConfigC(**good)), 0, C.byref(h)) == -2   # no GPU here
     assert L.fhe_bert_ready(None) == 0
+
+
+def test_gadget_group_validation():
+    """Every gadget's grouping factor (fast, fast2, mid, mid2) is 0, 1 or 2,
+    and a multi-bit (group 2) gadget needs N = 1024, k = 2, n <= 1023 and
+    level <= 8 (the 48-bit-accumulator kernels go to level 8); the oracle
+    library resolves the same plan for the planner's multi-bit mids."""
+    from dataclasses import replace
+    L = _lib.lib()
+    h = C.c_void_p()
+    p21 = params_for_bits(21)
+    assert (p21.pbs_mid_group, p21.pbs_mid2_group) == (2, 2)
+    P = _lib.params_struct(p21.as_dict())
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
+    L.fhe_ctx_destroy(h)
+    for field in ("pbs_fast_group", "pbs_fast2_group", "pbs_mid_group", "pbs_mid2_group"):
+        P = _lib.params_struct(dict(p21.as_dict(), **{field: 3}))
+        assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1, field
+        assert b"must be 0, 1 or 2" in L.fhe_last_error(None)
+    toy_mid = replace(TOY, msg_bits=11, pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_level=2,
+                      pbs_mid_base_log=10, pbs_mid_level=2, pbs_mid_group=2)
+    P = _lib.params_struct(toy_mid.as_dict())
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1
+    assert b"multi-bit blind rotation (group 2) needs N = 1024" in L.fhe_last_error(None)
+    deep = dict(p21.as_dict(), pbs_mid_base_log=4, pbs_mid_level=9)
+    P = _lib.params_struct(deep)
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1
