@@ -147,7 +147,7 @@ static int validate(const fhe_params* p, std::string& why) {
     const int bl = g == 1 ? p->pbs_fast_base_log : g == 2 ? p->pbs_fast2_base_log
                                                           : g == 3 ? p->pbs_mid_base_log : p->pbs_mid2_base_log;
     if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group / pbs_mid_group / pbs_mid2_group must be 0, 1 or 2"; return -1; }
-    (void)bl;  // 32-bit accumulators when level <= 2 and level * base_log <= 31, else 64-bit (k_blind_rotate_mb64)
+    (void)bl;  // 32-bit accumulators when level <= 2 and level * base_log <= 31, else 48-bit (k_blind_rotate_mb64)
     if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 8)) {
       why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 8";
       return -1;
@@ -1039,7 +1039,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
       name = "k_blind_rotate_mb<DBG>";
     } else
 #endif
-    // 64-bit accumulators (L * beta > 31 or L > 2): the deep gadgets
+    // wide (48-bit) accumulators (L * beta > 31 or L > 2): the deep gadgets
     if (!(p.pbs_level <= 2 && p.pbs_level * p.pbs_base_log <= 31)) {
 #define MB64(L)                                                                                                  \
   hipLaunchKernelGGL((k_blind_rotate_mb64<L, 0>), gm, bm, 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft,   \

@@ -58,7 +58,7 @@ class SchemeParams:
     pbs_mid2_base_log: int = 0
     pbs_mid2_level: int = 0
     # grouping factor of the mid / mid2 gadget's blind rotation (as
-    # pbs_fast_group; 2 = multi-bit, 64-bit accumulators past level 2)
+    # pbs_fast_group; 2 = multi-bit, 48-bit accumulators past level 2)
     pbs_mid_group: int = 0
     pbs_mid2_group: int = 0
 

@@ -81,7 +81,7 @@ typedef struct fhe_params {
                                 Their keys: fhe_export_fast_bsk which = 3, 4. */
   int32_t pbs_mid_group;     /* grouping factor of the mid / mid2 gadget's blind */
   int32_t pbs_mid2_group;    /* rotation, as pbs_fast_group: 2 = multi-bit (levels
-                                up to 8; 64-bit accumulators past level 2 or
+                                up to 8; 48-bit accumulators past level 2 or
                                 level * base_log > 31: k_blind_rotate_mb64) */
 } fhe_params;
 
