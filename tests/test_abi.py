@@ -203,3 +203,20 @@ def test_gadget_group_validation():
     deep = dict(p21.as_dict(), pbs_mid_base_log=4, pbs_mid_level=9)
     P = _lib.params_struct(deep)
     assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1
+
+
+def test_every_planned_parameter_set_validates():
+    """params_for_bits(P) for every supported width yields a set the library
+    accepts (host context), with the same sign plan as params.py."""
+    L = _lib.lib()
+    h = C.c_void_p()
+    for P in range(1, 28):
+        p = params_for_bits(P)
+        cp = _lib.params_struct(p.as_dict())
+        assert L.fhe_ctx_create(C.byref(cp), -1, C.byref(h)) == 0, (P, L.fhe_last_error(None))
+        L.fhe_ctx_destroy(h)
+        if P >= 4:
+            sched = (C.c_int32 * 64)()
+            R = L.fhe_sign_schedule(C.byref(cp), sched, 64)
+            from fheicp.params import sign_schedule
+            assert list(sched[:R]) == sign_schedule(p)[1], P
