@@ -334,6 +334,19 @@ __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, i
   fold8<true>(v);
 }
 
+// the inverse from layout LB on (after the C -> B relayout's writes and reads,
+// which a caller may have split between waves)
+template <int DBG = 0, int NR = 0>
+__device__ __forceinline__ void inverse_post(c64 (&v)[S], const c64* twl, int lane, c64 wf = {},
+                                             const c64* treg = nullptr) {
+  lane_tw<1, true, DBG>(v, twl, lane, wf);
+  idft8(v);
+  if constexpr ((DBG & 8) == 0) swap_lb(v);
+  lane_tw<0, true, DBG, NR>(v, twl, lane, wf, treg);
+  idft8(v);
+  fold8<true>(v);
+}
+
 // ---- accumulator word type ------------------------------------------------
 template <bool A32>
 struct Acc;

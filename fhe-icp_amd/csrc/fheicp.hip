@@ -594,7 +594,7 @@ static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* b
     case 1024:
       if (variant_for(ctx, p) == 4 || words)
         hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, bsk, npoly, ctx->tw4,
-                           bsk_fft, 1.0 / 18446744073709551616.0 / (double)(p.N / 2));
+                           bsk_fft, 1.0 / 18446744073709551616.0 / (double)(p.N / 2), words && mb_xpose(p.pbs_level) ? 1 : 0);
 #ifdef FHEICP_AB
       else if (variant_for(ctx, p) == 3)
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);

@@ -291,9 +291,14 @@ __global__ void __launch_bounds__(V::NT, MINW) k_blind_rotate_mw(const u64* __re
 // of the forward transform) and scaled by 1/M.
 // scale = 2^-64 / M: both accumulator widths (br_v4.h Acc) read the torus
 // from z - floor(z) or z - rint(z), so the products arrive already scaled
+// perm != 0 (the multi-bit keys of the gadgets mb_rotate runs with mb_xpose): the
+// value of output point (slot u, lane) goes to [2 (lane >> 4) + (u & 1)]
+// [16 (u >> 1) + (lane & 15)], so the product wave of quarter g, which loads
+// key slot 2g + t at its lane l, gets point (slot 2 (l >> 4) + t, lane
+// 16 g + (l & 15)).
 __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bsk, int npoly,
                                                       const c64* __restrict__ tw4, c64* __restrict__ out,
-                                                      double scale) {
+                                                      double scale, int perm) {
   using namespace v4;
   __shared__ c64 twl[NTW];
   __shared__ c64 scr[SCR];
@@ -312,7 +317,10 @@ __global__ void __launch_bounds__(64) k_bsk_to_fft_v4(const u64* __restrict__ bs
     forward(v, twl, scr, lane);
     c64* dst = out + (size_t)poly * M;
 #pragma unroll
-    for (int u = 0; u < S; ++u) dst[u * 64 + lane] = {v[u].x * inv, v[u].y * inv};
+    for (int u = 0; u < S; ++u) {
+      const int pos = perm ? (2 * (lane >> 4) + (u & 1)) * 64 + 16 * (u >> 1) + (lane & 15) : u * 64 + lane;
+      dst[pos] = {v[u].x * inv, v[u].y * inv};
+    }
   }
 }
 
@@ -672,6 +680,18 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
 // - 1) factors, one inverse: about the work of one classic step for two LWE
 // coefficients, at half the barriers.
 namespace fhei {
+// The product wave of quarter g works on source lanes 16g..16g+15, all eight
+// slots (lane l: slots 2 (l >> 4) + t), so that after its products two lane
+// swaps give each lane all eight slots of one ciphertext: the wave runs the
+// inverse's first DFT-8 pass itself and writes straight to the owner's
+// relayout positions (8 LDS stores and 8 reads per wave and pair fewer).
+// 0: quarter = slots 2g, 2g+1 of all lanes, products handed off as they are.
+// Level-1 gadgets only (mb_xpose): mb<1,0,23> -1.0 to -1.5% per launch, while
+// mb<2,0,15> was unchanged and mb64<4> 2.7% slower (docs/AB_LOG_r03.md).
+#ifndef FHEICP_MB_XPOSE
+#define FHEICP_MB_XPOSE 1
+#endif
+__host__ __device__ constexpr bool mb_xpose(int level) { return FHEICP_MB_XPOSE == 2 || (FHEICP_MB_XPOSE == 1 && level == 1); }
 namespace mb {
 constexpr int NP_MAX = (v4::NMAX + 1) / 2;  // pairs
 __host__ __device__ constexpr int bitrev9(int j) {
@@ -780,7 +800,12 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   // this wave's product quarter: slots 2g, 2g+1; the exponent of slot 2g in
   // 16-byte units, so a * eb16 holds the table entry's byte offset (before
   // the swizzle) in bits 4-14
-  const uint32_t eb16 = (((uint32_t)mb::exponent(lane, 0) + 256u * bitrev3(2 * g)) & 2047u) << 4;
+  constexpr bool XP = mb_xpose(L);
+  const uint32_t eb16 = XP
+                            ? ((uint32_t)mb::exponent(16 * g + (lane & 15), 2 * (lane >> 4)) & 2047u) << 4
+                            : (((uint32_t)mb::exponent(lane, 0) + 256u * bitrev3(2 * g)) & 2047u) << 4;
+  // this lane's F position in the slot regions for t = 0 (+ 64 t)
+  const int fpos = XP ? 2 * (lane >> 4) * 64 + 16 * g + (lane & 15) : 0;
 
   // the offset of decompose_v4's offset form (wide accumulators carry it)
   const int prec = L * bta;
@@ -922,7 +947,7 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
         for (int gg = 0; gg < G; ++gg) {
           c64 F[WPC];
 #pragma unroll
-          for (int r = 0; r < WPC; ++r) F[r] = xbuf[(gg * WPC + r) * SCR + u * 64 + lane];
+          for (int r = 0; r < WPC; ++r) F[r] = xbuf[(gg * WPC + r) * SCR + (XP ? fpos + t * 64 : u * 64 + lane)];
 #pragma unroll
           for (int Ss = 0; Ss < 3; ++Ss) {
             c64 P = {0.0, 0.0};
@@ -944,18 +969,41 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
       lds_barrier();
       MB_PRIO(3);
     }
-    // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
-#pragma unroll
-    for (int gg = 0; gg < G; ++gg)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) xbuf[(gg * WPC + comp) * SCR + (2 * g + t) * 64 + lane] = o[gg][t];
-    lds_barrier();
-    MB_PRIO(3);
-    V4_STAMP(10);
     c64 ov[S];
+    if constexpr (XP) {
+      // lane 16 q + s holds o[gg][t] = ciphertext gg, slot 2q + t of source
+      // lane 16 g + s; exchanging q with gg (permlane32 / permlane16 swaps)
+      // gives lane 16 gg + s the eight slots of ciphertext gg, on which this
+      // wave runs the inverse's first pass and writes the owner's relayout
 #pragma unroll
-    for (int u = 0; u < S; ++u) ov[u] = slot[u * 64 + lane];
-    inverse<0, NR>(ov, twl, slot, lane, {}, treg);
+      for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) ov[2 * gg + t] = o[gg][t];
+      swap_bit<0, 4>(ov);
+      swap_bit<1, 2>(ov);
+      idft8(ov);
+      c64* own = xbuf + ((lane >> 4) * WPC + comp) * SCR + rpos(R2I, jof(LC, 16 * g + (lane & 15), 0));
+#pragma unroll
+      for (int u = 0; u < S; ++u) own[rpos(R2I, jof(LC, 0, u))] = ov[u];
+      lds_barrier();
+      MB_PRIO(3);
+      V4_STAMP(10);
+#pragma unroll
+      for (int u = 0; u < S; ++u) ov[u] = slot[rpos(R2I, jof(LB, lane, u))];
+      inverse_post<0, NR>(ov, twl, lane, {}, treg);
+    } else {
+      // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) xbuf[(gg * WPC + comp) * SCR + (2 * g + t) * 64 + lane] = o[gg][t];
+      lds_barrier();
+      MB_PRIO(3);
+      V4_STAMP(10);
+#pragma unroll
+      for (int u = 0; u < S; ++u) ov[u] = slot[u * 64 + lane];
+      inverse<0, NR>(ov, twl, slot, lane, {}, treg);
+    }
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       if constexpr (A48) {
