@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-compares", type=int, default=0,
-                    help="oracle sample size (0: 32 compares scaled down by the sign plan's cost, 10-30 s)")
+                    help="oracle sample size (0: 64 compares scaled down by the sign plan's cost, 10-30 s)")
     ap.add_argument("--mode", choices=("compare", "corpus", "embed"), default="compare",
                     help="compare: the reference's path (configs[1]); corpus: search over a stored corpus of "
                          "seeded-LWE documents (SURVEY.md §8f-1); embed: the BERT encoder of the embedding "
@@ -495,13 +495,13 @@ def topk_check(args, model, world, oa, oi):
 
 
 def cpu_sample(args, p) -> int:
-    """Compares timed on the CPU oracle: --cpu-compares, or 32 at the
-    headline's plan cost (5.6 relative bootstraps, about 11 s on 16 host
+    """Compares timed on the CPU oracle: --cpu-compares, or 64 at the
+    headline's plan cost (3.9 relative bootstraps, about 12 s on 16 host
     threads) scaled down to the configuration's plan, at least 8."""
     if args.cpu_compares:
         return args.cpu_compares
     from fheicp.params import plan_cost
-    return int(max(8, min(32, round(32 * 5.6 / max(plan_cost(p), 1e-9)))))
+    return int(max(8, min(64, round(64 * 3.9 / max(plan_cost(p), 1e-9)))))
 
 
 def shard_parity(args, model, q_np, docs_np, acc_dev, below_dev, T) -> dict:
