@@ -35,10 +35,12 @@ enum { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_RESID_F32 = 2 };
 // erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
 // rounding of the GELU output): one reciprocal, one exp and five FMAs against
 // the library erff's ~3x the instructions, which made the FFN GEMM's epilogue
-// as long as its main loop
+// as long as its main loop. The reciprocal is the hardware v_rcp_f32 (1 ulp):
+// __frcp_rn's correctly rounded form is a ten-instruction division sequence
+// (div_scale x2, div_fmas, div_fixup, FMAs) per element.
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
   const float p = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
                        0.254829592f) * t;
   return copysignf(1.0f - p * __expf(-ax * ax), x);
