@@ -191,7 +191,7 @@ static void gemm3_launch(const bf16* A, const bf16* W, const float* bias, const 
 }
 
 // ---- fused attention (flash-style) ------------------------------------------
-// One workgroup per (sequence, head) and 64 query rows; 4 waves of 16 rows.
+// One workgroup per (sequence, head) and 128 query rows (k_attention<8>; 64 rows of 4 waves beyond 256 tokens), 16 rows per wave.
 // K ([Sp][72]) and V transposed ([64][Sp + 8]) of the head are staged in LDS
 // once; each wave walks the keys in chunks of 64: S = Q K^T by MFMA (scale
 // 1/8, key mask as -inf), online softmax (running max and sum per row), P
@@ -211,19 +211,24 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
-__global__ void __launch_bounds__(256) k_attention(const bf16* __restrict__ qkv, const int32_t* __restrict__ mask,
-                                                   bf16* __restrict__ ctx, int S, int Sp, int nh, int H) {
+// NW waves of 16 query rows each: 8 (128 rows) up to Sp = 256, so a
+// sequence of <= 128 tokens stages its head's K and V once instead of once per
+// 64 query rows; 4 beyond (the LDS of Sp = 512).
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) k_attention(const bf16* __restrict__ qkv, const int32_t* __restrict__ mask,
+                                                       bf16* __restrict__ ctx, int S, int Sp, int nh, int H) {
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int VLD = Sp + 8;
   bf16* Ks = reinterpret_cast<bf16*>(smem);       // [Sp][KLD]
   bf16* Vt = Ks + Sp * KLD;                        // [HD][VLD]
-  bf16* Ps = Vt + HD * VLD;                        // [4][16][KLD]
-  float* madd = reinterpret_cast<float*>(Ps + 4 * 16 * KLD);  // [Sp]
+  bf16* Ps = Vt + HD * VLD;                        // [NW][16][KLD]
+  float* madd = reinterpret_cast<float*>(Ps + NW * 16 * KLD);  // [Sp]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int b = blockIdx.x / nh, h = blockIdx.x - b * nh;
   const int H3 = 3 * H;
   const bf16* base = qkv + (size_t)b * S * H3 + h * HD;
-  for (int idx = tid; idx < Sp * 8; idx += 256) {
+  for (int idx = tid; idx < Sp * 8; idx += NT) {
     const int s = idx >> 3, c = (idx & 7) * 8;
     uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
     if (s < S) {
@@ -235,9 +240,9 @@ __global__ void __launch_bounds__(256) k_attention(const bf16* __restrict__ qkv,
 #pragma unroll
     for (int j = 0; j < 8; ++j) Vt[(c + j) * VLD + s] = ve[j];
   }
-  for (int s = tid; s < Sp; s += 256) madd[s] = (s < S && mask[(size_t)b * S + s] != 0) ? 0.0f : -INFINITY;
+  for (int s = tid; s < Sp; s += NT) madd[s] = (s < S && mask[(size_t)b * S + s] != 0) ? 0.0f : -INFINITY;
   __syncthreads();
-  const int q0 = blockIdx.y * 64 + w * 16;
+  const int q0 = blockIdx.y * (16 * NW) + w * 16;
   if (q0 >= S) return;  // no barrier below
   const int qr = q0 + (l & 15);
   bf16x8 qa[2];
@@ -722,10 +727,12 @@ int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, c
   pend(h, h->p_other, st, e1, 0.0);
   BCHK(h, hipGetLastError());
   const int Sp = (S + 63) / 64 * 64;
-  const size_t attn_lds = (size_t)Sp * KLD * 2 + (size_t)HD * (Sp + 8) * 2 + 4 * 16 * KLD * 2 + (size_t)Sp * 4;
+  const int anw = Sp <= 256 ? 8 : 4;  // waves per attention workgroup (k_attention)
+  const size_t attn_lds = (size_t)Sp * KLD * 2 + (size_t)HD * (Sp + 8) * 2 + (size_t)anw * 16 * KLD * 2 + (size_t)Sp * 4;
   static bool attn_attr = false;
   if (!attn_attr) {
-    BCHK(h, hipFuncSetAttribute((const void*)k_attention, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    BCHK(h, hipFuncSetAttribute((const void*)k_attention<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    BCHK(h, hipFuncSetAttribute((const void*)k_attention<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attn_attr = true;
   }
   int rc;
@@ -733,8 +740,12 @@ int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, c
     const Layer& L = h->layers[li];
     if ((rc = gemm<EPI_BF16>(h, hb, L.wqkv, L.bqkv, nullptr, qkv, M, 3 * H, H, st))) return rc;
     pbegin(h, h->p_attn, st, &e1);
-    hipLaunchKernelGGL(k_attention, dim3((unsigned)(B * nh), (unsigned)(Sp / 64)), dim3(256), attn_lds, st, qkv,
-                       d_mask, ctx, S, Sp, nh, H);
+    if (anw == 8)
+      hipLaunchKernelGGL(k_attention<8>, dim3((unsigned)(B * nh), (unsigned)((Sp + 127) / 128)), dim3(512), attn_lds, st,
+                         qkv, d_mask, ctx, S, Sp, nh, H);
+    else
+      hipLaunchKernelGGL(k_attention<4>, dim3((unsigned)(B * nh), (unsigned)(Sp / 64)), dim3(256), attn_lds, st, qkv,
+                         d_mask, ctx, S, Sp, nh, H);
     pend(h, h->p_attn, st, e1, 4.0 * B * nh * (double)S * S * HD);
     BCHK(h, hipGetLastError());
     if ((rc = gemm<EPI_RESID_F32>(h, ctx, L.wo, L.bo, hs, tmp, M, H, H, st))) return rc;
