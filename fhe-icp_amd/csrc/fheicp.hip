@@ -147,9 +147,11 @@ static int validate(const fhe_params* p, std::string& why) {
     const int bl = g == 1 ? p->pbs_fast_base_log : g == 2 ? p->pbs_fast2_base_log
                                                           : g == 3 ? p->pbs_mid_base_log : p->pbs_mid2_base_log;
     if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group / pbs_mid_group / pbs_mid2_group must be 0, 1 or 2"; return -1; }
-    (void)bl;  // 32-bit accumulators when level <= 2 and level * base_log <= 31, else 48-bit (k_blind_rotate_mb64)
-    if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 8)) {
-      why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 8";
+    // 32-bit accumulators when level <= 2 and level * base_log <= 31, else
+    // 48-bit (k_blind_rotate_mb64), whose digits are read as 32-bit fields:
+    // base_log <= 31 (a wider digit's f64 products are noise anyway)
+    if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 8 && bl <= 31)) {
+      why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 8, base_log <= 31";
       return -1;
     }
   }

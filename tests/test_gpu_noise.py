@@ -52,6 +52,9 @@ INSTANCES = {
     (7, 6, 2): "k_blind_rotate_mb64<6, 0>",
     (6, 7, 2): "k_blind_rotate_mb64<7, 0>",
     (5, 8, 2): "k_blind_rotate_mb64<8, 0>",
+    # level 2 with L * beta > 31 also takes the 48-bit kernel (level 1 would
+    # need beta >= 32, which fhe_ctx_create refuses for multi-bit gadgets)
+    (16, 2, 2): "k_blind_rotate_mb64<2, 0>",
 }
 COUNT = 4096
 TV = 1 << 61
@@ -99,6 +102,15 @@ def test_bootstrap_noise_vs_model(need_gpu, oracle_lib, gadget):
     assert np.abs(ph[:2] - ph_ref).max() < 8 * sigma_model * 2.0 ** 64
     assert np.array_equal(ph_ref > 0, sgn[:2] > 0)
     eng.close()
+
+
+def test_multibit_digit_width_limit(need_gpu):
+    """A multi-bit gadget with 32-bit digits is refused at context creation
+    (the 48-bit kernel reads digits as 32-bit fields; measured before the
+    check: sigma 2^-2.2 against a model of 2^-5.6 for (32, 1))."""
+    from fheicp import _lib
+    with pytest.raises(_lib.FheError, match="base_log <= 31"):
+        Engine(SchemeParams(msg_bits=16, pbs_fast_base_log=32, pbs_fast_level=1, pbs_fast_group=2), 0)
 
 
 @pytest.mark.parametrize("ks", [(3, 5), (4, 4)])
