@@ -1,5 +1,5 @@
 #!/bin/bash
-# Closing pass on one GPU (tools/closing_r03.sh TAG (r03fin the last), outputs gpurun_out/TAG_*,
+# Closing pass on one GPU (tools/closing_r03.sh TAG (r03end the last), outputs gpurun_out/TAG_*,
 # copied to profiles/ by hand): the whole -m gpu suite, smoke, the PMC passes
 # of the headline, C3 (one stream) and C5 (tools/pmc_r03.sh; br_pmc.json keyed
 # on this build's sha256, installed for the bench lines that follow), the
@@ -7,7 +7,7 @@
 # stage, the SQ counters of the headline and C5 kernels, and a 2-rank gloo
 # rehearsal of the N > 1 (C4, 100k docs) path.
 set -u -o pipefail
-T=${1:-r03fin}
+T=${1:-r03end}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"; cd "$R"
 step() { echo "== $1 $(date +%T)" >> "$OUT/${T}_steps.log"; }
 step tests; timeout -k 10 900 python -u -m pytest tests/ -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/${T}_tests.log" 2>&1 || exit 1
