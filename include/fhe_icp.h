@@ -71,7 +71,7 @@ typedef struct fhe_params {
                               2 = multi-bit, pairs of coefficients with three GGSWs
                               each (fhe_export_fast_bsk's layout: [pair][subset][row]
                               [component][coef]); needs N = 1024, k = 2, n <= 1023,
-                              level <= 8 */
+                              level <= 8, base_log <= 31 */
   int32_t pbs_mid_base_log;  /* optional gadgets between the main and the fast one */
   int32_t pbs_mid_level;     /* (0, 0: none; classic rotation; mid needs the fast  */
   int32_t pbs_mid2_base_log; /* gadget, mid2 needs mid): the sign plan runs the     */
