@@ -221,3 +221,21 @@ def test_every_planned_parameter_set_validates():
             R = L.fhe_sign_schedule(C.byref(cp), sched, 64)
             from fheicp.params import sign_schedule
             assert list(sched[:R]) == sign_schedule(p)[1], P
+
+
+def test_multibit_digit_width_validation():
+    """Multi-bit gadgets read their digits as 32-bit fields in the 48-bit
+    kernel: base_log > 31 is refused at context creation (host-only contexts
+    validate too); the classic rotation and narrower multi-bit gadgets pass."""
+    L = _lib.lib()
+    h = C.c_void_p()
+    base = params_for_bits(16).as_dict()
+    P = _lib.params_struct(dict(base, pbs_fast2_base_log=32, pbs_fast2_level=1, pbs_fast2_group=2))
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1
+    assert b"base_log <= 31" in L.fhe_last_error(None)
+    assert L.fhe_sign_pbs_count(C.byref(P)) == -1
+    for ok in (dict(base, pbs_fast2_base_log=31, pbs_fast2_level=1, pbs_fast2_group=2),
+               dict(base, pbs_fast_base_log=16, pbs_fast_level=2, pbs_fast_group=2)):
+        P = _lib.params_struct(ok)
+        assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0 and h.value
+        L.fhe_ctx_destroy(h)
