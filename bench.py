@@ -16,8 +16,10 @@ exchange step of the sharded search) plus the merge.
 Inputs (query, documents) are resident in HBM before the timed region.
 value = compares processed by all ranks / (max over ranks of the time).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL = backend "nccl").
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either
+under torch.distributed.run (one process per GPU, RCCL = backend "nccl";
+WORLD_SIZE must equal --gpus), or directly: the process then starts the N
+ranks itself (launch_ranks) and relays rank 0's line.
 """
 from __future__ import annotations
 
@@ -70,6 +72,54 @@ def parse():
     ap.add_argument("--embed-batch", type=int, default=256, help="--mode embed: sequences per forward pass")
     ap.add_argument("--seq-len", type=int, default=100, help="--mode embed: tokens per sequence (max_length)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_cmd(gpus: int, argv: list[str]) -> list[str]:
+    """The torch.distributed.run line that starts one rank per GPU on this
+    node (the driver's own form, rendezvous on 127.0.0.1), forwarding argv."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+            str(Path(__file__).resolve())] + list(argv)
+
+
+def launch_ranks(args, argv: list[str]) -> int | None:
+    """--gpus N against the process layout, before anything touches the GPU.
+
+    Under a launcher (WORLD_SIZE set) the world must be --gpus: a mismatch
+    exits non-zero instead of measuring another GPU count. Invoked directly
+    with --gpus N > 1, this process starts the N ranks itself as a child
+    torch.distributed.run (no exec: it never initialises the GPU) and returns
+    the child's exit code; rank 0's JSON line reaches stdout unchanged.
+    None: this process is the (only) rank."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if args.gpus == 1:
+        return None
+    import signal
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    child = subprocess.Popen(rank_launch_cmd(args.gpus, argv), env=env)
+    # forward a termination to the launcher, which stops its ranks
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda s, _f: child.send_signal(s))
+    return child.wait()
 
 
 def dist_setup(args):
@@ -310,6 +360,9 @@ def roofline(p, brs, batch: int = 0, iso: dict | None = None) -> dict:
 
 def main():
     args = parse()
+    code = launch_ranks(args, sys.argv[1:])
+    if code is not None:
+        sys.exit(code)
     world, rank, local = dist_setup(args)
     if args.workload == "auto":
         args.workload = "c4" if world > 1 else "c2"
@@ -524,17 +577,16 @@ def shard_parity(args, model, q_np, docs_np, acc_dev, below_dev, T) -> dict:
 
 
 def time_allgather(k, dev, on_dev, iters=20) -> float:
-    """Mean time of the search's one exchange step (the all-gather of k
-    (acc, index) pairs per rank, fheicp.search.sharded_topk), after the timed
+    """Mean time of the search's one exchange step (one all-gather of k
+    (acc, index) pairs per rank packed as [k, 2] int64, fheicp.search.sharded_topk), after the timed
     region so it does not perturb it."""
-    a = torch.zeros(k, dtype=torch.int64, device=dev if on_dev else "cpu")
+    a = torch.zeros(k, 2, dtype=torch.int64, device=dev if on_dev else "cpu")
     world = torch.distributed.get_world_size()
     outs = [torch.empty_like(a) for _ in range(world)]
     torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        torch.distributed.all_gather(outs, a)
         torch.distributed.all_gather(outs, a)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / iters * 1e3

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/fhe_icp.h"
+#include "../../include/fhe_icp_dev.h"
 #include "common.h"
 #include "k_client.h"
 #include "k_server.h"
@@ -114,6 +115,13 @@ static int validate(const fhe_params* p, std::string& why) {
     why = "ks decomposition out of range (base_log <= 7 for int8 digits)"; return -1;
   }
   if (p->msg_bits < 2 || p->msg_bits > 40) { why = "msg_bits must be in [2, 40]"; return -1; }
+  // the key switch's tie coins are input bits 62 - prec - j (j < ks_level),
+  // fair only above the zero bits a shifted input brings in: the sign
+  // extraction shifts by up to msg_bits - 1 (sign_rounds)
+  if (p->ks_level * p->ks_base_log + p->ks_level + p->msg_bits > 64) {
+    why = "ks_level * (ks_base_log + 1) + msg_bits must be <= 64 (key-switch tie coins above every shift)";
+    return -1;
+  }
   if (p->lwe_noise_bits < 0 || p->lwe_noise_bits > 60 || p->glwe_noise_bits < 0 || p->glwe_noise_bits > 60) {
     why = "noise bits out of range"; return -1;
   }
@@ -152,6 +160,12 @@ static int validate(const fhe_params* p, std::string& why) {
     // base_log <= 31 (a wider digit's f64 products are noise anyway)
     if (grp == 2 && L && !(p->N == 1024 && p->k == 2 && p->n <= 1023 && L <= 8 && bl <= 31)) {
       why = "multi-bit blind rotation (group 2) needs N = 1024, k = 2, n <= 1023, level <= 8, base_log <= 31";
+      return -1;
+    }
+    // the 48-bit words keep bits 16-63: every digit field and the rounding
+    // bit 2^(63 - L*beta) must lie there, so L * beta <= 47
+    if (grp == 2 && L && !(L <= 2 && L * bl <= 31) && L * bl > 47) {
+      why = "multi-bit blind rotation (group 2) on 48-bit accumulators needs level * base_log <= 47";
       return -1;
     }
   }
@@ -917,12 +931,15 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
   return FHE_OK;
 }
 
+// largest input shift whose key-switch tie coins (bits 62 - prec - j of the
+// shifted input, j < ks_level) are all input bits, not the zeros shifted in
+static int ks_max_shift(const fhe_params& p) { return 63 - p.ks_level * p.ks_base_log - p.ks_level; }
 int fhe_keyswitch_batch(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, int32_t shift, uint64_t add_body,
                         uint64_t* d_small, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
-  if (count < 0 || shift < 0 || shift > 63 || (count > 0 && (!d_big || !d_small)))
-    return fail(ctx, FHE_E_ARG, "bad keyswitch arguments");
+  if (count < 0 || shift < 0 || shift > ks_max_shift(ctx->p) || (count > 0 && (!d_big || !d_small)))
+    return fail(ctx, FHE_E_ARG, "bad keyswitch arguments (shift must be in [0, 63 - ks_level * (ks_base_log + 1)])");
   if (count == 0) return FHE_OK;
   return keyswitch_lane(ctx, d_big, count, shift, add_body, d_small, (hipStream_t)stream, 0);
 }

@@ -856,7 +856,8 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
     if constexpr (A48) {
       uint32_t t = s < S ? alo[s] : alo[s - S];
       asm volatile("" : "+v"(t));  // unpacked per level, not hoisted out of the loop as 8 more VGPRs
-      w = ((u64)acc[s] << 32) | (s < S ? t << 16 : t);  // bits 0-15 unused (fields start >= 16)
+      // bits 0-15 unused: fields start at 64 - L*beta >= 17 (validate() refuses L*beta > 47 here)
+      w = ((u64)acc[s] << 32) | (s < S ? t << 16 : t);
     } else {
       w = (u64)acc[s];
     }

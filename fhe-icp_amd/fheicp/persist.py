@@ -21,8 +21,11 @@ This file format makes a model reproducible across processes and GPUs
 The password comes from ``password=`` or ``$FHE_MASTER_PASSWORD``; without
 one, saving secret keys raises unless ``allow_plaintext_secrets=True`` (then
 s_small / s_big are stored as plain uint64 arrays, as version-1 files did).
-Version 2 is the format with the Fernet-wrapped ``secret`` blob; version-1
-files (plaintext s_small / s_big) still load. ``load_model(..., keys=False)``
+Version 2 marks the format with the Fernet-wrapped ``secret`` blob. Files
+an earlier release wrote as version 1 hold either plaintext s_small / s_big
+or, when it was given a password, that same ``secret`` blob under the same
+``meta["secret"]`` entry: both still load (``_read_secrets`` goes by whether
+the blob is present, not by the version). ``load_model(..., keys=False)``
 reads only the quantisation and scheme (the clear modes need no secret).
 """
 from __future__ import annotations
@@ -38,7 +41,7 @@ from .model import QuantParams
 from .params import SchemeParams
 
 FORMAT = "fheicp-model"
-VERSION = 2                 # 2: Fernet-wrapped "secret" blob; 1: plaintext secret keys
+VERSION = 2                 # 2: Fernet-wrapped "secret" blob; 1: plaintext keys or the same blob
 KEY_NAMES = ("s_small", "s_big", "bsk", "ksk")
 SECRET_NAMES = ("s_small", "s_big")
 KDF_ITERATIONS = 100_000
@@ -117,8 +120,6 @@ def _check_version(path: str, meta: dict, supported: int) -> None:
     v = int(meta.get("version", 0))
     if not 1 <= v <= supported:
         raise ValueError(f"{path}: format version {meta.get('version')} is not supported (1..{supported})")
-    if v == 1 and "secret" in meta:
-        raise ValueError(f"{path}: version-1 file with an encrypted secret blob (corrupt)")
 
 
 def load_model(path: str, password: str | None = None, keys: bool = True):

@@ -24,16 +24,18 @@ def sharded_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx
     oa, oi = topk_fn(acc, below, k, base_idx)
     if world == 1:
         return oa, oi
+    # one collective: the k (acc, index) pairs travel packed as [k, 2] int64.
     # RCCL gathers device tensors in place; other backends (gloo rehearsals)
     # go through host copies
     dev = oa.device
     host = dev.type != "cpu" and torch.distributed.get_backend(group) != "nccl"
-    sa, si = (oa.cpu(), oi.cpu()) if host else (oa, oi)
-    ga = [torch.empty_like(sa) for _ in range(world)]
-    gi = [torch.empty_like(si) for _ in range(world)]
-    torch.distributed.all_gather(ga, sa, group=group)
-    torch.distributed.all_gather(gi, si, group=group)
-    cat_a, cat_i = torch.cat(ga).to(dev), torch.cat(gi).to(dev)
+    pairs = torch.stack([oa.to(torch.int64), oi.to(torch.int64)], dim=1)
+    if host:
+        pairs = pairs.cpu()
+    gathered = [torch.empty_like(pairs) for _ in range(world)]
+    torch.distributed.all_gather(gathered, pairs, group=group)
+    cat = torch.cat(gathered).to(dev)
+    cat_a, cat_i = cat[:, 0].contiguous(), cat[:, 1].contiguous()
     ma, pos = topk_fn(cat_a, (cat_i < 0).to(torch.int64), k, 0)
     mi = torch.where(pos >= 0, cat_i[pos.clamp(min=0)], pos)
     return ma, mi

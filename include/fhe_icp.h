@@ -336,12 +336,6 @@ int fhe_profile_kernel_name(fhe_ctx* ctx, const char* kernel, char* h_buf, size_
 /* "libfheicp gfx950 ab=0" for the shipped build; ab=1 for A/B builds
  * (tools/build_variant.sh -DFHEICP_AB: extra v4 shapes, v3, timing kernels). */
 const char* fhe_build_info(void);
-/* Development aid (A/B builds only; FHE_E_STATE otherwise): 4 x 16 s_memtime
- * phase stamps of one wave of the v4 blind rotation, then 2048 x {start, end,
- * HW_ID} per workgroup (s_memrealtime), recorded only when FHEICP_V4_DBG=128
- * (tools/prof_br.py --stamps); h_out holds 64 + 6144 words. */
-int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out);
-
 #ifdef __cplusplus
 }
 #endif

@@ -465,9 +465,11 @@ void ref_decompose(uint64_t x, int bl, int L, int64_t* d) { decompose(x, bl, L, 
  * uniform x they are fair and independent of the rounded value: every
  * digit is then zero-mean with E[d^2] = (B^2 + 2) / 12, the noise model's
  * factor, where digits in [-B/2, B/2) have mean -1/2 and put a
- * key-dependent bias 0.5 * sum(KSK noise) on every key switch. (Needs
- * prec + L <= 63, and the bits are fair only above any shift of the
- * input: prec + L - 1 < 62 - shift; fhe_ctx_create checks the first.) */
+ * key-dependent bias 0.5 * sum(KSK noise) on every key switch. (The lowest
+ * coin, bit 63 - prec - L, must lie at or above any shift of the input:
+ * shift <= 63 - prec - L. fhe_ctx_create checks prec + L + msg_bits <= 64,
+ * the sign extraction shifting by at most msg_bits - 1, and
+ * fhe_keyswitch_batch refuses larger shifts.) */
 static void decompose_ks(uint64_t x, int bl, int L, int64_t* d) {
   const int prec = L * bl;
   uint64_t v = ((x >> (63 - prec)) + 1) >> 1;

@@ -239,3 +239,24 @@ def test_multibit_digit_width_validation():
         P = _lib.params_struct(ok)
         assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0 and h.value
         L.fhe_ctx_destroy(h)
+
+
+def test_wide_multibit_and_ks_coin_bounds():
+    """Two parameter bounds checked at context creation (host-only contexts
+    validate too): a multi-bit gadget on the 48-bit accumulators needs
+    level * base_log <= 47 (its digit fields and rounding bit live in bits
+    16-63), and the key switch's tie coins must sit above every shift of the
+    sign extraction: ks_level * (ks_base_log + 1) + msg_bits <= 64."""
+    L = _lib.lib()
+    h = C.c_void_p()
+    base = params_for_bits(16).as_dict()
+    for bad, msg in ((dict(base, pbs_mid_base_log=12, pbs_mid_level=4, pbs_mid_group=2), b"<= 47"),
+                     (dict(base, ks_base_log=7, ks_level=7, msg_bits=16), b"msg_bits must be <= 64")):
+        P = _lib.params_struct(bad)
+        assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1
+        assert msg in L.fhe_last_error(None), L.fhe_last_error(None)
+    for ok in (dict(base, pbs_mid_base_log=15, pbs_mid_level=3, pbs_mid_group=2),
+               dict(base, ks_base_log=7, ks_level=6, msg_bits=16)):
+        P = _lib.params_struct(ok)
+        assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0 and h.value
+        L.fhe_ctx_destroy(h)

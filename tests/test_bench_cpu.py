@@ -1,0 +1,72 @@
+"""Host-only checks of bench.py's launch contract (no GPU): --gpus must agree
+with the launcher's WORLD_SIZE, and a direct `--gpus N` run starts N ranks
+itself through torch.distributed.run (rendezvous on 127.0.0.1)."""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def test_world_size_mismatch_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "8", "--steps", "1"],
+                       cwd=str(REPO), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "--gpus 8 but WORLD_SIZE=2" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_rank_launch_cmd():
+    sys.path.insert(0, str(REPO))
+    import bench
+    cmd = bench.rank_launch_cmd(4, ["--gpus", "4", "--steps", "3"])
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert int(cmd[cmd.index("--master-port") + 1]) > 0
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert cmd[-5] == str(REPO / "bench.py")
+
+
+def test_packed_allgather_gloo_two_ranks(tmp_path):
+    """The sharded top-k's single all-gather of packed [k, 2] pairs on a gloo
+    world of 2 (the exchange bench.py and BatchProcessor use)."""
+    code = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from fheicp.search import sharded_topk, host_topk
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo")
+calls = []
+orig = dist.all_gather
+def counting(*a, **k):
+    calls.append(a[1].shape)
+    return orig(*a, **k)
+dist.all_gather = counting
+acc = torch.tensor([5, 9, 9, 1] if rank == 0 else [9, 7, 5, 9], dtype=torch.int64)
+below = torch.zeros(4, dtype=torch.int64)
+oa, oi = sharded_topk(acc, below, 3, rank * 4, host_topk, 2)
+assert len(calls) == 1 and tuple(calls[0]) == (3, 2), calls
+assert oa.tolist() == [9, 9, 9] and oi.tolist() == [1, 2, 4], (oa, oi)
+dist.destroy_process_group()
+print("ok", rank)
+"""
+    script = tmp_path / "ag.py"
+    script.write_text(code)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(script),
+           str(REPO / "fhe-icp_amd")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "ok 0" in r.stdout and "ok 1" in r.stdout
+
+
+def _port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p

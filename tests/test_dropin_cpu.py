@@ -370,6 +370,38 @@ def test_persist_versions(tmp_path):
                 persist.load_model(path)
 
 
+def test_persist_v1_with_password_blob_loads(tmp_path, monkeypatch):
+    """The release before version 2 (da9f35f) wrote VERSION = 1 together with
+    the Fernet-wrapped `secret` blob whenever a password was set. Such a file
+    (rebuilt here byte for byte: the same arrays, meta version 1) loads with
+    the password, and without one under keys=False (the clear modes)."""
+    import json
+    from fheicp import persist
+    from fheicp.params import params_for_bits
+    from fheicp.sklearn import LinearRegression
+    monkeypatch.delenv("FHE_MASTER_PASSWORD", raising=False)
+    X, y = _data(16)
+    qp = LinearRegression(n_bits=6).fit(X, y).quant_params
+    sch = params_for_bits(qp.msg_bits())
+    keys = {k: np.arange(20, dtype=np.uint64) % 2 for k in persist.KEY_NAMES}
+    path = str(tmp_path / "v1.npz")
+    persist.save_model(path, qp, sch, keys, password="pw")
+    with np.load(path) as z:
+        arrays = {k: z[k].copy() for k in z.files}
+    meta = json.loads(bytes(arrays["meta"]).decode())
+    assert "secret" in meta and "secret" in arrays
+    meta["version"] = 1
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez(path, **arrays)
+    _, _, k2 = persist.load_model(path, password="pw")
+    for k in persist.KEY_NAMES:
+        np.testing.assert_array_equal(k2[k], keys[k])
+    q2, s2, none = persist.load_model(path, keys=False)
+    assert none is None and q2.to_dict() == qp.to_dict() and s2 == sch
+    with pytest.raises(ValueError, match="password"):
+        persist.load_model(path)
+
+
 def test_corpus_secret_checked_before_keygen(tmp_path, monkeypatch):
     """A processor that will save an encrypted corpus refuses to start without
     a password (or the plaintext opt-in) before any training or keygen."""

@@ -133,3 +133,24 @@ def test_bench_c4_two_ranks_gloo(need_gpu, tmp_path):
     assert par["acc_bit_exact"] and par["threshold_bit_exact"] and par["quant_params_equal"]
     assert out["topk_check"]["indices_equal"] and out["topk_check"]["scores_equal"]
     assert out["allgather_ms"] >= 0
+
+
+def test_bench_gpus2_without_launcher(need_gpu):
+    """`python bench.py --gpus 2` exactly as the driver invokes the N = 1 line
+    (no torch.distributed.run, no WORLD_SIZE): bench.py must start the two
+    ranks itself, and the line must be a 2-rank measurement with per-rank
+    parity and the merged top-10 checked (gloo ranks sharing GPU 0)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(FHEICP_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--workload", "c4", "--total-docs", "4096",
+           "--steps", "1", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=str(REPO), env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "shard2"
+    par = out["parity"]
+    assert par["ranks"] == 2 and par["compares_checked"] == 4096
+    assert par["acc_bit_exact"] and par["threshold_bit_exact"] and par["quant_params_equal"]
+    assert out["topk_check"]["indices_equal"] and out["topk_check"]["scores_equal"]
