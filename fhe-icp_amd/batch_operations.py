@@ -54,6 +54,9 @@ FHE_MODES = ("execute", "simulate", "disable")
 # which reducer produced a stored vector (BatchConfig.gpu_reducer)
 REDUCER_KEY = "fheicp_reducer"
 GPU_REDUCER = "gpu-pca-f64"
+# which encoder embedded it (BatchConfig.gpu_embedder; absent: the reference's
+# torch fp32 forward), e.g. "hip-bert-f32" (fheicp.bert.GpuBert.provenance)
+EMBEDDER_KEY = "fheicp_embedder"
 
 
 @dataclass
@@ -82,6 +85,16 @@ class BatchConfig:
     # allow_mixed_reducers, and are bit-exact within one reducer's vectors.
     gpu_reducer: bool = False
     allow_mixed_reducers: bool = False
+    # run the BERT encoder of the default BertEmbedder in libfheicp
+    # (fheicp.bert, §8f-4) instead of the reference's torch fp32 forward:
+    # gpu_embedder_precision "f32" (the reference's arithmetic on the f32
+    # MFMA, another summation order) or "bf16". Not bit-equal to torch, so
+    # the same contract as gpu_reducer: stored vectors carry
+    # metadata[EMBEDDER_KEY] = the encoder's provenance, and scores never mix
+    # encoders (ValueError) unless allow_mixed_embedders.
+    gpu_embedder: bool = False
+    gpu_embedder_precision: str = "f32"
+    allow_mixed_embedders: bool = False
     key_manager_default: bool = True  # no key_manager given: FHEKeyManager() as the reference (:64)
     device: int = 0
     model_path: Optional[str] = None  # fheicp.persist file: load instead of retrain (§8f-2)
@@ -112,6 +125,8 @@ class BatchConfig:
             raise ValueError("search_chunk must be >= 1")
         if self.input_dim < 1 or not 2 <= self.n_bits <= 16:
             raise ValueError("input_dim must be >= 1 and n_bits in [2, 16]")
+        if self.gpu_embedder_precision not in ("f32", "bf16"):
+            raise ValueError("gpu_embedder_precision must be 'f32' or 'bf16'")
 
 
 def _world():
@@ -278,10 +293,13 @@ class BatchProcessor:
         """The embedder and reducer, created as the reference does on first
         use (:62-63): ``bert_embeddings.BertEmbedder()`` and
         ``dimension_reduction.DimensionReducer.load(config.reducer_path)``
-        from the reference's modules on sys.path."""
+        from the reference's modules on sys.path (with config.gpu_embedder the
+        BertEmbedder mirror runs libfheicp's encoder)."""
         if self.embedder is None:
             from bert_embeddings import BertEmbedder
-            self.embedder = BertEmbedder()
+            cfg = self.config
+            self.embedder = (BertEmbedder(gpu_encoder=True, gpu_precision=cfg.gpu_embedder_precision)
+                             if cfg.gpu_embedder else BertEmbedder())
         if self.reducer is None:
             from dimension_reduction import DimensionReducer
             self.reducer = DimensionReducer.load(self.config.reducer_path)
@@ -294,12 +312,24 @@ class BatchProcessor:
         embedder, reducer = self._upstream()
         return reducer.transform(embedder.get_embeddings_batch(texts))
 
+    def _tags(self) -> Dict[str, Optional[str]]:
+        """Provenance of the vectors this processor makes from text: the
+        reducer (GPU PCA or not) and the encoder (None: torch fp32)."""
+        embedder, _ = self._upstream()
+        return {REDUCER_KEY: GPU_REDUCER if self.config.gpu_reducer else None,
+                EMBEDDER_KEY: getattr(embedder, "provenance", None)}
+
+    @staticmethod
+    def _tagged(meta: List[Dict], tags: Dict[str, Optional[str]]) -> List[Dict]:
+        set_ = {k: v for k, v in tags.items() if v is not None}
+        return [dict(m, **set_) for m in meta] if set_ else meta
+
     def encrypt_documents(self, texts: List[str], doc_ids: Optional[List[str]] = None,
                           metadata: Optional[List[Dict]] = None) -> List[str]:
         """Embed, reduce and store documents (:120-204): one index rewrite per batch."""
         self._require_model()
-        self._check_reducers(list(self.storage.index.keys()), GPU_REDUCER if self.config.gpu_reducer else None,
-                             query=True)
+        tags = self._tags()
+        self._check_provenance(list(self.storage.index.keys()), tags)
         n = len(texts)
         if doc_ids is None:
             stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
@@ -312,9 +342,7 @@ class BatchProcessor:
             if self._check_memory() > self.config.max_memory_mb:
                 self._maybe_gc()
             vecs = self._embed(texts[s:e])
-            meta = metadata[s:e]
-            if self.config.gpu_reducer:
-                meta = [dict(m, **{REDUCER_KEY: GPU_REDUCER}) for m in meta]
+            meta = self._tagged(metadata[s:e], tags)
             docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs, key_id, meta)
             self.storage.save_many(docs)
             out.extend(d.doc_id for d in docs)
@@ -338,10 +366,22 @@ class BatchProcessor:
                                   timestamp=stamp, encrypted_embedding=payloads[i], model_version=version,
                                   key_id=key_id, metadata=metadata[i]) for i in range(len(doc_ids))]
 
+    _CONFIG = object()
+
     def store_vectors(self, vecs: np.ndarray, doc_ids: List[str], texts: Optional[List[str]] = None,
-                      metadata: Optional[List[Dict]] = None) -> List[str]:
-        """encrypt_documents for already reduced vectors (no embedder needed)."""
+                      metadata: Optional[List[Dict]] = None, reducer=_CONFIG,
+                      embedder: Optional[str] = None) -> List[str]:
+        """encrypt_documents for already reduced vectors (no embedder needed).
+
+        ``reducer`` / ``embedder`` name where the vectors came from, for the
+        provenance contract (default: the config's reducer, GPU_REDUCER under
+        gpu_reducer; the reference's torch encoder); they are tagged and
+        checked against the store as in encrypt_documents."""
         self._require_model()
+        if reducer is BatchProcessor._CONFIG:
+            reducer = GPU_REDUCER if self.config.gpu_reducer else None
+        tags = {REDUCER_KEY: reducer, EMBEDDER_KEY: embedder}
+        self._check_provenance(list(self.storage.index.keys()), tags)
         n = len(doc_ids)
         texts = texts if texts is not None else list(doc_ids)
         metadata = metadata if metadata is not None else [{} for _ in range(n)]
@@ -349,30 +389,38 @@ class BatchProcessor:
         out: List[str] = []
         for s in range(0, n, self.config.batch_size):
             e = min(n, s + self.config.batch_size)
-            docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs[s:e], key_id, metadata[s:e])
+            meta = self._tagged(metadata[s:e], tags)
+            docs = self._make_documents(texts[s:e], doc_ids[s:e], vecs[s:e], key_id, meta)
             self.storage.save_many(docs)
             out.extend(d.doc_id for d in docs)
         return out
 
-    def _reducer_of(self, doc_id: str):
-        return self.storage.index[doc_id].get("metadata", {}).get(REDUCER_KEY)
+    def _tag_of(self, doc_id: str, key: str):
+        return self.storage.index[doc_id].get("metadata", {}).get(key)
 
-    def _check_reducers(self, doc_ids, query_reducer=None, query: bool = False):
-        """The GPU-PCA contract (BatchConfig.gpu_reducer): the vectors that
-        meet in one score come from one reducer."""
-        if self.config.allow_mixed_reducers:
-            return
-        seen = {self._reducer_of(i) for i in doc_ids if i in self.storage.index}
-        if query:
-            seen.add(query_reducer)
-        if len(seen) > 1:
-            raise ValueError(f"vectors from different dimension reducers {sorted(map(str, seen))} would meet in one "
-                             "score: the GPU and CPU PCA differ at quantizer rounding boundaries "
-                             "(BatchConfig.gpu_reducer, allow_mixed_reducers)")
+    def _check_provenance(self, doc_ids, query_tags: Optional[Dict[str, Optional[str]]] = None):
+        """The GPU-stage contract (BatchConfig.gpu_reducer, gpu_embedder): the
+        vectors that meet in one score come from one reducer and one encoder.
+        A GPU stage is not bit-equal to the CPU one it replaces, and a feature
+        on the other side of an input-quantizer rounding boundary changes the
+        accumulator; within one provenance every score is the oracle's."""
+        what = ((REDUCER_KEY, "dimension reducers", "the GPU and CPU PCA", "gpu_reducer", "allow_mixed_reducers"),
+                (EMBEDDER_KEY, "embedders", "the HIP and torch BERT encoders", "gpu_embedder",
+                 "allow_mixed_embedders"))
+        for key, name, pair, knob, allow in what:
+            if getattr(self.config, allow):
+                continue
+            seen = {self._tag_of(i, key) for i in doc_ids if i in self.storage.index}
+            if query_tags is not None:
+                seen.add(query_tags.get(key))
+            if len(seen) > 1:
+                raise ValueError(f"vectors from different {name} {sorted(map(str, seen))} would meet in one "
+                                 f"score: {pair} differ at quantizer rounding boundaries "
+                                 f"(BatchConfig.{knob}, {allow})")
 
     def compare_encrypted(self, doc_id1: str, doc_id2: str) -> float:
         self._require_model()
-        self._check_reducers([doc_id1, doc_id2])
+        self._check_provenance([doc_id1, doc_id2])
         d1, d2 = self.storage.load(doc_id1), self.storage.load(doc_id2)
         if self.storage.holds_ciphertexts() or d1.model_version != "1.0" or d2.model_version != "1.0":
             return self._compare_ciphertexts(d1, d2)
@@ -403,8 +451,7 @@ class BatchProcessor:
     def search_similar(self, query_text: str, top_k: int = 5, min_similarity: float = 0.5) -> List[Tuple[str, float]]:
         self._require_model()
         embedder, reducer = self._upstream()
-        self._check_reducers(list(self.storage.index.keys()),
-                             GPU_REDUCER if self.config.gpu_reducer else None, query=True)
+        self._check_provenance(list(self.storage.index.keys()), self._tags())
         q = embedder.get_embedding(query_text)
         q = reducer.transform(np.asarray(q).reshape(1, -1))[0]
         return self.search_vector(q, top_k, min_similarity)

@@ -5,11 +5,16 @@ Same class, arguments, results and errors as the reference's
 a ``transformers`` BERT loaded by name (:42-47), ``get_embedding`` /
 ``get_embeddings_batch`` with mean / cls / max pooling over
 ``last_hidden_state`` (:53-158, padding=True, truncation at max_length),
-``compute_similarity`` (:160-178). What changes is where the forward pass
-runs: on a GPU device the model's weights go once into libfheicp's encoder
-(fheicp.bert.GpuBert: bf16 MFMA GEMMs, fused attention, fp32 LayerNorm and
-pooling; include/fhe_bert.h) and every batch runs there; device="cpu" keeps
-the torch model, as the reference does on a host without CUDA.
+``compute_similarity`` (:160-178).
+
+By default the forward pass is the reference's own: the torch model in fp32
+on ``device`` (:46, :136). ``gpu_encoder=True`` moves it into libfheicp's
+encoder on a GPU device (fheicp.bert.GpuBert): ``gpu_precision="f32"``
+(default) keeps the reference's arithmetic on the f32 MFMA in another
+summation order, ``"bf16"`` rounds the GEMM operands to bf16. Either way the
+embeddings are not bit-equal to torch's, so ``provenance`` names the encoder
+(None for torch) and batch_operations tags stored vectors with it and refuses
+to score vectors of different encoders together.
 
 ``model=`` / ``tokenizer=`` take already-built objects (the weights and the
 vocabulary are downloads the offline image does not have).
@@ -30,7 +35,7 @@ class BertEmbedder:
     """Extract BERT embeddings for text documents."""
 
     def __init__(self, model_name: str = 'bert-base-uncased', max_length: int = 100, device: Optional[str] = None,
-                 model=None, tokenizer=None):
+                 model=None, tokenizer=None, gpu_encoder: bool = False, gpu_precision: str = 'f32'):
         import torch
         self.model_name = model_name
         self.max_length = min(max_length, 512)  # BERT's limit (:30)
@@ -50,13 +55,20 @@ class BertEmbedder:
         self.model.eval()
         self.hidden_size = self.model.config.hidden_size
         self.gpu = None
-        if str(self.device).startswith('cuda'):
+        if gpu_encoder:
+            if not str(self.device).startswith('cuda'):
+                raise ValueError("gpu_encoder=True needs a cuda device")
             from fheicp.bert import GpuBert
             idx = torch.device(self.device).index
-            self.gpu = GpuBert(model=self.model, device=0 if idx is None else idx)
+            self.gpu = GpuBert(model=self.model, device=0 if idx is None else idx, precision=gpu_precision)
         else:
             self.model.to(self.device)
         logger.info(f"Model loaded. Hidden size: {self.hidden_size}")
+
+    @property
+    def provenance(self) -> Optional[str]:
+        """None for the reference's torch forward, else the HIP encoder's tag."""
+        return self.gpu.provenance if self.gpu is not None else None
 
     def _pooled(self, encoded, pooling: str) -> np.ndarray:
         if pooling not in POOLINGS:

@@ -190,6 +190,146 @@ static void gemm3_launch(const bf16* A, const bf16* W, const float* bias, const 
                      tiles_n, nblk);
 }
 
+// ---- GEMM in the reference's arithmetic: f32 operands, f32 MFMA ----------
+// The same block structure with fp32 A and W: v_mfma_f32_32x32x2_f32 is an
+// exact f32 fma chain (one rounding per product, f32 accumulation), i.e. the
+// arithmetic of torch's fp32 Linear, in another summation order. K step 32
+// keeps the 128-byte rows of the bf16 kernel (eight 16-byte chunks, the same
+// XOR swizzle and LDS-DMA pieces), so the staging is byte-for-byte the one
+// above. Each wave owns 64 x 64 outputs as 2 x 2 tiles of 32 x 32; W is the
+// MFMA's A operand (D = W . A^T: a lane holds four consecutive output columns
+// per register group). Within a K step the MFMA's two k slots take the
+// halves of the 32-wide step (lane half h supplies k = 16 h + t at step t),
+// so a lane's operands are 64 contiguous bytes of one row: four b128 reads.
+constexpr int F_BK = 32, F_STAGE = (BM + G3_BN) * F_BK;  // floats per stage (48 KB)
+constexpr int F_LDS = 3 * F_STAGE * (int)sizeof(float);  // 147456 B
+enum { EPI_F32 = 3, EPI_GELU_F32 = 4 };                   // (+ EPI_RESID_F32)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// BERT's exact GELU in f32 (x * 0.5 * (1 + erf(x / sqrt(2))), transformers'
+// GELUActivation): the library erff, not the bf16 path's 1.5e-7 approximation
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, const float* __restrict__ W,
+                                                   const float* __restrict__ bias, const float* __restrict__ resid,
+                                                   float* __restrict__ out, int M, int N, int K, int tiles_n,
+                                                   int nblk) {
+  constexpr int BN = G3_BN, WN = 2;  // 8 waves in 4 x 2, each 64 x 64
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* st = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, l = tid & 63, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w - wm * WN;
+  const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * BN;
+  const int KT = K / F_BK;
+  auto issue = [&](int kt, int s) {
+    float* la = st + s * F_STAGE;
+    float* lb = la + BM * F_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // A: 32 pieces of 8 rows x 128 B, four per wave
+      const int pc = 4 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+      const int gm = min(m0 + row, M - 1);  // rows past M: loaded, never stored
+      __builtin_amdgcn_global_load_lds(A + (size_t)gm * K + kt * F_BK + 4 * c, (lds_void*)(la + pc * 8 * F_BK), 16, 0,
+                                       0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // W: 16 pieces, two per wave
+      const int pc = 2 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+      const int gn = min(n0 + row, N - 1);
+      __builtin_amdgcn_global_load_lds(W + (size_t)gn * K + kt * F_BK + 4 * c, (lds_void*)(lb + pc * 8 * F_BK), 16, 0,
+                                       0);
+    }
+  };
+  f32x16 acc[2][2];  // [n tile][m tile]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  issue(0, 0);
+  if (KT > 1) issue(1, 1);
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + 1 < KT)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < KT) issue(kt + 2, (kt + 2) % 3);
+    const float* la = st + (kt % 3) * F_STAGE;
+    const float* lb = la + BM * F_BK;
+    float4 wv[2][4], av[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = wn * 64 + 32 * j + (l & 31), m = wm * 64 + 32 * j + (l & 31);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        wv[j][u] = *reinterpret_cast<const float4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
+        av[j][u] = *reinterpret_cast<const float4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i][u][e], av[j][u][e], acc[i][j], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's reads retire before the next barrier
+  }
+  // epilogue through LDS as k_gemm3: the wave's 64 x 64 tile row-major in a
+  // private region (pitch 68 floats), then whole 256-byte row pieces
+  __syncthreads();
+  const int colw = n0 + wn * 64, roww = m0 + wm * 64;
+  if (colw >= N) return;
+  constexpr int EPL = 68;
+  float* ep = reinterpret_cast<float*>(smem) + (size_t)w * (64 * EPL);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int c = 32 * i + 8 * gq + 4 * h;  // four consecutive output columns of register group gq
+      const float4 bv4 = *reinterpret_cast<const float4*>(bias + colw + c);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rl = 32 * j + (l & 31);
+        float v[4] = {acc[i][j][4 * gq] + bv4.x, acc[i][j][4 * gq + 1] + bv4.y, acc[i][j][4 * gq + 2] + bv4.z,
+                      acc[i][j][4 * gq + 3] + bv4.w};
+        if constexpr (EPI == EPI_GELU_F32) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) v[rr] = gelu_erf(v[rr]);
+        }
+        *reinterpret_cast<float4*>(ep + rl * EPL + c) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int pc = l + 64 * it, rl = pc >> 4, cp = pc & 15;
+    const int row = roww + rl;
+    if (row >= M) continue;
+    float4 v = *reinterpret_cast<const float4*>(ep + rl * EPL + 4 * cp);
+    const size_t o = (size_t)row * N + colw + 4 * cp;
+    if constexpr (EPI == EPI_RESID_F32) {
+      const float4 rs = *reinterpret_cast<const float4*>(resid + o);
+      v = make_float4(v.x + rs.x, v.y + rs.y, v.z + rs.z, v.w + rs.w);
+    }
+    *reinterpret_cast<float4*>(out + o) = v;
+  }
+}
+
+template <int EPI>
+static void gemm3_f32_launch(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
+                             int N, int K, hipStream_t st) {
+  const int tiles_n = (N + G3_BN - 1) / G3_BN, nblk = tiles_n * ((M + BM - 1) / BM);
+  hipLaunchKernelGGL(k_gemm3_f32<EPI>, dim3((unsigned)nblk), dim3(512), F_LDS, st, A, W, bias, resid, out, M, N, K,
+                     tiles_n, nblk);
+}
+
 // ---- fused attention (flash-style) ------------------------------------------
 // One workgroup per (sequence, head) and 128 query rows (k_attention<8>; 64 rows of 4 waves beyond 256 tokens), 16 rows per wave.
 // K ([Sp][72]) and V transposed ([64][Sp + 8]) of the head are staged in LDS
@@ -322,6 +462,113 @@ __global__ void __launch_bounds__(NW * 64) k_attention(const bf16* __restrict__ 
   }
 }
 
+// ---- attention in f32 (the reference's arithmetic) --------------------------
+// One workgroup per (sequence, head, 128 query rows), four waves of 32 rows.
+// Keys stream through LDS in blocks of 64 (K and V rows, pitch 68 floats).
+// Per 32-key tile a wave forms S^T = K . Q^T on v_mfma_f32_32x32x2_f32 (key on
+// the register, query on the lane: lane half h takes head dims 32 h + t at
+// step t, its Q row slice lives in 32 VGPRs), so the softmax's per-query max
+// and sum run over a lane's own registers plus one xor-32 exchange, and P^T
+// stays in registers as the B operand of O^T += V^T . P^T (register r of the
+// S^T tile is the k slot of one MFMA: keys (r & 3) + 8 (r >> 2) + 4 h).
+// Scale 1/8 and the mask (-inf) as BertSelfAttention; f32 exp.
+constexpr int FA_KB = 64, FA_LD = HD + 4;
+
+__global__ void __launch_bounds__(256) k_attention_f32(const float* __restrict__ qkv, const int32_t* __restrict__ mask,
+                                                       float* __restrict__ ctx, int S, int nh, int H) {
+  __shared__ __attribute__((aligned(16))) float Ks[FA_KB * FA_LD];
+  __shared__ __attribute__((aligned(16))) float Vs[FA_KB * FA_LD];
+  __shared__ float madd[FA_KB];
+  const int tid = threadIdx.x, l = tid & 63, h = l >> 5, w = tid >> 6;
+  const int b = blockIdx.x / nh, hd = blockIdx.x - b * nh;
+  const int H3 = 3 * H;
+  const float* base = qkv + (size_t)b * S * H3 + hd * HD;
+  const int q0 = blockIdx.y * 128 + w * 32, qr = q0 + (l & 31);
+  float qv[32];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const float4 z = qr < S ? *reinterpret_cast<const float4*>(base + (size_t)qr * H3 + 32 * h + 4 * u)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    qv[4 * u] = z.x, qv[4 * u + 1] = z.y, qv[4 * u + 2] = z.z, qv[4 * u + 3] = z.w;
+  }
+  float m = -INFINITY, lsum = 0.0f;
+  f32x16 o[2];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.0f;
+  for (int k0 = 0; k0 < S; k0 += FA_KB) {
+    __syncthreads();  // the previous block's reads are done
+    for (int idx = tid; idx < FA_KB * 16; idx += 256) {
+      const int s = idx >> 4, c = (idx & 15) * 4;
+      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+      if (k0 + s < S) {
+        kv = *reinterpret_cast<const float4*>(base + (size_t)(k0 + s) * H3 + H + c);
+        vv = *reinterpret_cast<const float4*>(base + (size_t)(k0 + s) * H3 + 2 * H + c);
+      }
+      *reinterpret_cast<float4*>(Ks + s * FA_LD + c) = kv;
+      *reinterpret_cast<float4*>(Vs + s * FA_LD + c) = vv;
+    }
+    if (tid < FA_KB) madd[tid] = (k0 + tid < S && mask[(size_t)b * S + k0 + tid] != 0) ? 0.0f : -INFINITY;
+    __syncthreads();
+    if (q0 >= S) continue;  // no work, but this wave keeps joining the barriers
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s[kt][e] = 0.0f;
+      const float* kr = Ks + (32 * kt + (l & 31)) * FA_LD + 32 * h;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 kk = *reinterpret_cast<const float4*>(kr + 4 * u);
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.x, qv[4 * u], s[kt], 0, 0, 0);
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.y, qv[4 * u + 1], s[kt], 0, 0, 0);
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.z, qv[4 * u + 2], s[kt], 0, 0, 0);
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.w, qv[4 * u + 3], s[kt], 0, 0, 0);
+      }
+    }
+    float mc = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int key = 32 * kt + (e & 3) + 8 * (e >> 2) + 4 * h;
+        s[kt][e] = s[kt][e] * 0.125f + madd[key];
+        mc = fmaxf(mc, s[kt][e]);
+      }
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    const float mn = fmaxf(m, mc);  // block 0 holds key 0 ([CLS], never masked): finite from it on
+    const float alpha = expf(m - mn);
+    m = mn;
+    float ps = 0.0f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s[kt][e] = expf(s[kt][e] - mn);
+        ps += s[kt][e];
+      }
+    lsum = lsum * alpha + ps;  // this lane half's keys; the halves meet at the end
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[0][e] *= alpha, o[1][e] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float* vr = Vs + (32 * kt + (e & 3) + 8 * (e >> 2) + 4 * h) * FA_LD + (l & 31);
+        o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[0], s[kt][e], o[0], 0, 0, 0);
+        o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr[32], s[kt][e], o[1], 0, 0, 0);
+      }
+  }
+  if (qr >= S) return;
+  const float inv = 1.0f / (lsum + __shfl_xor(lsum, 32, 64));
+  float* dst = ctx + ((size_t)b * S + qr) * H + hd * HD;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq)
+      *reinterpret_cast<float4*>(dst + 32 * dt + 8 * gq + 4 * h) =
+          make_float4(o[dt][4 * gq] * inv, o[dt][4 * gq + 1] * inv, o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+}
+
 // ---- LayerNorm, embeddings, pooling ------------------------------------------
 // one wave per row of H <= 1024 (H / 64 values per lane), fp32 two-pass
 // mean / variance as torch.nn.functional.layer_norm (biased variance)
@@ -346,7 +593,7 @@ __device__ __forceinline__ void ln_row(float (&v)[LN_MAXV], int nv, const float*
     const int c = j * 64 + l;
     const float r = (v[j] - mean) * rstd * g[c] + be[c];
     y[c] = r;
-    yb[c] = (bf16)r;
+    if (yb) yb[c] = (bf16)r;  // the bf16 GEMM input (bf16 arithmetic only)
   }
 }
 
@@ -358,7 +605,7 @@ __global__ void __launch_bounds__(256) k_layernorm(const float* __restrict__ x, 
   const int nv = H / 64;
   float v[LN_MAXV];
   for (int j = 0; j < nv; ++j) v[j] = x[(size_t)row * H + j * 64 + l];
-  ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb + (size_t)row * H, H);
+  ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb ? yb + (size_t)row * H : nullptr, H);
 }
 
 // the same LayerNorm with 16-byte accesses (H % 256 == 0): lane l holds
@@ -396,7 +643,7 @@ __global__ void __launch_bounds__(256) k_layernorm4(const float* __restrict__ x,
                                  (v[j].z - mean) * rstd * gg.z + bb.z, (v[j].w - mean) * rstd * gg.w + bb.w);
     *reinterpret_cast<float4*>(y + (size_t)row * H + c) = r;
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    *reinterpret_cast<bf16x4*>(yb + (size_t)row * H + c) = (bf16x4){(bf16)r.x, (bf16)r.y, (bf16)r.z, (bf16)r.w};
+    if (yb) *reinterpret_cast<bf16x4*>(yb + (size_t)row * H + c) = (bf16x4){(bf16)r.x, (bf16)r.y, (bf16)r.z, (bf16)r.w};
   }
 }
 
@@ -418,7 +665,7 @@ __global__ void __launch_bounds__(256) k_embed_ln(const int32_t* __restrict__ id
     const int c = j * 64 + l;
     v[j] = we[(size_t)id * H + c] + te[(size_t)t * H + c] + pe[(size_t)s * H + c];
   }
-  ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb + (size_t)row * H, H);
+  ln_row(v, nv, g, be, eps, l, y + (size_t)row * H, yb ? yb + (size_t)row * H : nullptr, H);
 }
 
 // bert_embeddings.py:140-149: mean over the attention mask, [CLS], or max over
@@ -453,7 +700,8 @@ using namespace fbert;
 
 namespace {
 struct Layer {
-  bf16 *wqkv = nullptr, *wo = nullptr, *wi = nullptr, *wo2 = nullptr;
+  bf16 *wqkv = nullptr, *wo = nullptr, *wi = nullptr, *wo2 = nullptr;      // FHE_BERT_BF16
+  float *fqkv = nullptr, *fo = nullptr, *fi = nullptr, *fo2 = nullptr;     // FHE_BERT_F32
   float *bqkv = nullptr, *bo = nullptr, *bi = nullptr, *bo2 = nullptr;
   float *ln1w = nullptr, *ln1b = nullptr, *ln2w = nullptr, *ln2b = nullptr;
 };
@@ -467,6 +715,7 @@ struct Prof {
 struct fhe_bert {
   fhe_bert_config cfg{};
   int device = -1;
+  int precision = FHE_BERT_F32;  // the reference's arithmetic unless set otherwise before any tensor
   std::string err;
   float *we = nullptr, *pe = nullptr, *te = nullptr, *elnw = nullptr, *elnb = nullptr;
   std::vector<Layer> layers;
@@ -511,9 +760,37 @@ int fhe_bert_create(const fhe_bert_config* c, int device, fhe_bert** out) {
   h->device = device;
   h->layers.resize(c->num_layers);
   h->have.assign(c->num_layers + 1, 0);
+  // the >64 KB dynamic-LDS attribute of the kernels that need it, set on this
+  // handle's device (the attribute is per device; every handle sets it)
+  int rc = FHE_OK;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_gemm3<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm3<EPI_GELU_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm3<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_GELU_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS) ||
+      hipFuncSetAttribute((const void*)k_attention<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ||
+      hipFuncSetAttribute((const void*)k_attention<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
+    rc = FHE_E_DEVICE;
+  if (rc) {
+    delete h;
+    return rc;
+  }
   *out = h;
   return FHE_OK;
 }
+
+int fhe_bert_set_precision(fhe_bert* h, int32_t precision) {
+  if (!h) return FHE_E_ARG;
+  if (precision != FHE_BERT_F32 && precision != FHE_BERT_BF16) return bfail(h, FHE_E_ARG, "unknown precision");
+  for (uint64_t m : h->have)
+    if (m) return bfail(h, FHE_E_STATE, "set the precision before loading any tensor");
+  h->precision = precision;
+  return FHE_OK;
+}
+
+int fhe_bert_get_precision(const fhe_bert* h) { return h ? h->precision : FHE_E_ARG; }
 
 static void free_all(fhe_bert* h) {
   auto f = [](void* p) {
@@ -522,6 +799,7 @@ static void free_all(fhe_bert* h) {
   f(h->we), f(h->pe), f(h->te), f(h->elnw), f(h->elnb), f(h->ws);
   for (auto& L : h->layers) {
     f(L.wqkv), f(L.wo), f(L.wi), f(L.wo2), f(L.bqkv), f(L.bo), f(L.bi), f(L.bo2);
+    f(L.fqkv), f(L.fo), f(L.fi), f(L.fo2);
     f(L.ln1w), f(L.ln1b), f(L.ln2w), f(L.ln2b);
   }
   for (Prof* p : {&h->p_gemm, &h->p_attn, &h->p_other})
@@ -570,7 +848,9 @@ int fhe_bert_set_tensor(fhe_bert* h, int32_t layer, int32_t which, const float* 
   }
   if (layer >= c.num_layers) return bfail(h, FHE_E_ARG, "layer out of range");
   Layer& L = h->layers[layer];
-  // GEMM weights -> bf16; Q, K and V stack into one [3H][H] matrix
+  // GEMM weights -> bf16 (FHE_BERT_BF16) or as given (FHE_BERT_F32); Q, K and
+  // V stack into one [3H][H] matrix
+  const bool f32 = h->precision == FHE_BERT_F32;
   auto put_bf16 = [&](bf16** dst, size_t total, size_t off, int64_t n) -> int {
     if ((rc = want(n))) return rc;
     std::vector<uint16_t> t((size_t)n);
@@ -585,20 +865,23 @@ int fhe_bert_set_tensor(fhe_bert* h, int32_t layer, int32_t which, const float* 
     BCHK(h, hipMemcpy(*dst + off, data, (size_t)n * 4, hipMemcpyHostToDevice));
     return FHE_OK;
   };
+  auto put_w = [&](bf16** db, float** df, size_t total, size_t off, int64_t n) -> int {
+    return f32 ? put_f32(df, total, off, n) : put_bf16(db, total, off, n);
+  };
   switch (which) {
-    case FHE_BERT_Q_W: rc = put_bf16(&L.wqkv, 3 * H * H, 0, H * H); break;
-    case FHE_BERT_K_W: rc = put_bf16(&L.wqkv, 3 * H * H, H * H, H * H); break;
-    case FHE_BERT_V_W: rc = put_bf16(&L.wqkv, 3 * H * H, 2 * H * H, H * H); break;
+    case FHE_BERT_Q_W: rc = put_w(&L.wqkv, &L.fqkv, 3 * H * H, 0, H * H); break;
+    case FHE_BERT_K_W: rc = put_w(&L.wqkv, &L.fqkv, 3 * H * H, H * H, H * H); break;
+    case FHE_BERT_V_W: rc = put_w(&L.wqkv, &L.fqkv, 3 * H * H, 2 * H * H, H * H); break;
     case FHE_BERT_Q_B: rc = put_f32(&L.bqkv, 3 * H, 0, H); break;
     case FHE_BERT_K_B: rc = put_f32(&L.bqkv, 3 * H, H, H); break;
     case FHE_BERT_V_B: rc = put_f32(&L.bqkv, 3 * H, 2 * H, H); break;
-    case FHE_BERT_AO_W: rc = put_bf16(&L.wo, H * H, 0, H * H); break;
+    case FHE_BERT_AO_W: rc = put_w(&L.wo, &L.fo, H * H, 0, H * H); break;
     case FHE_BERT_AO_B: rc = put_f32(&L.bo, H, 0, H); break;
     case FHE_BERT_AO_LN_W: rc = put_f32(&L.ln1w, H, 0, H); break;
     case FHE_BERT_AO_LN_B: rc = put_f32(&L.ln1b, H, 0, H); break;
-    case FHE_BERT_I_W: rc = put_bf16(&L.wi, I * H, 0, I * H); break;
+    case FHE_BERT_I_W: rc = put_w(&L.wi, &L.fi, I * H, 0, I * H); break;
     case FHE_BERT_I_B: rc = put_f32(&L.bi, I, 0, I); break;
-    case FHE_BERT_O_W: rc = put_bf16(&L.wo2, H * I, 0, H * I); break;
+    case FHE_BERT_O_W: rc = put_w(&L.wo2, &L.fo2, H * I, 0, H * I); break;
     case FHE_BERT_O_B: rc = put_f32(&L.bo2, H, 0, H); break;
     case FHE_BERT_O_LN_W: rc = put_f32(&L.ln2w, H, 0, H); break;
     case FHE_BERT_O_LN_B: rc = put_f32(&L.ln2b, H, 0, H); break;
@@ -670,11 +953,6 @@ int fhe_bert_profile_read(fhe_bert* h, const char* kernel, double* total_ms, int
 template <int EPI>
 static int gemm(fhe_bert* h, const bf16* A, const bf16* W, const float* bias, const float* resid, void* out, int M,
                 int N, int K, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    BCHK(h, hipFuncSetAttribute((const void*)k_gemm3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS));
-    attr = true;
-  }
   hipEvent_t e1;
   pbegin(h, h->p_gemm, st, &e1);
   // the three-stage LDS-DMA form everywhere (tools/gemm_probe.hip against the
@@ -685,56 +963,75 @@ static int gemm(fhe_bert* h, const bf16* A, const bf16* W, const float* bias, co
   return FHE_OK;
 }
 
-int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, const int32_t* d_mask, int32_t B,
-                     int32_t S, int32_t pooling, float* d_out, void* stream) {
-  if (!h) return FHE_E_ARG;
+template <int EPI>
+static int gemm_f32(fhe_bert* h, const float* A, const float* W, const float* bias, const float* resid, float* out,
+                    int M, int N, int K, hipStream_t st) {
+  hipEvent_t e1;
+  pbegin(h, h->p_gemm, st, &e1);
+  gemm3_f32_launch<EPI>(A, W, bias, resid, out, M, N, K, st);
+  pend(h, h->p_gemm, st, e1, 2.0 * M * N * K);
+  BCHK(h, hipGetLastError());
+  return FHE_OK;
+}
+
+static int layernorm(fhe_bert* h, const float* x, const float* g, const float* b, float* y, bf16* yb, int M, int H,
+                     float eps, hipStream_t st) {
+  hipEvent_t e1;
+  const unsigned rows4 = (unsigned)((M + 3) / 4);
+  pbegin(h, h->p_other, st, &e1);
+  if (H % 256 == 0)
+    hipLaunchKernelGGL(k_layernorm4, dim3(rows4), dim3(256), 0, st, x, g, b, y, yb, M, H, eps);
+  else
+    hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, x, g, b, y, yb, M, H, eps);
+  pend(h, h->p_other, st, e1, 0.0);
+  BCHK(h, hipGetLastError());
+  return FHE_OK;
+}
+
+// the f32 forward (FHE_BERT_F32): every GEMM and the attention on f32 MFMA,
+// workspace h | tmp | qkv | ctx | inter, all f32
+static int forward_f32(fhe_bert* h, const int32_t* d_mask, int B, int S, float* hs, hipStream_t st) {
   const fhe_bert_config& c = h->cfg;
-  if (B < 0 || S < 1 || S > c.max_position || pooling < 0 || pooling > FHE_BERT_POOL_NONE ||
-      (B > 0 && (!d_ids || !d_mask || !d_out)))
-    return bfail(h, FHE_E_ARG, "bad forward arguments (1 <= S <= max_position)");
-  if (!fhe_bert_ready(h)) return bfail(h, FHE_E_STATE, "weights not loaded (fhe_bert_set_tensor)");
-  if (B == 0) return FHE_OK;
-  BCHK(h, hipSetDevice(h->device));
-  hipStream_t st = (hipStream_t)stream;
-  const int H = c.hidden_size, I = c.intermediate_size, nh = c.num_heads;
-  const int64_t M64 = (int64_t)B * S;
-  if (M64 > (1 << 24)) return bfail(h, FHE_E_ARG, "B * S too large: split the call");
-  const int M = (int)M64;
-  // workspace: h f32 | tmp f32 | hb bf16 | qkv bf16 | ctx bf16 | inter bf16
-  const size_t need = (size_t)M * (4 * H + 4 * H + 2 * H + 6 * H + 2 * H + 2 * I);
-  if (need > h->ws_bytes) {
-    if (h->ws) {
-      BCHK(h, hipDeviceSynchronize());
-      BCHK(h, hipFree(h->ws));
-      h->ws = nullptr;
-      h->ws_bytes = 0;
-    }
-    BCHK(h, hipMalloc(&h->ws, need));
-    h->ws_bytes = need;
+  const int H = c.hidden_size, I = c.intermediate_size, nh = c.num_heads, M = B * S;
+  float* tmp = hs + (size_t)M * H;
+  float* qkv = tmp + (size_t)M * H;
+  float* ctx = qkv + (size_t)M * 3 * H;
+  float* inter = ctx + (size_t)M * H;
+  const float eps = c.layer_norm_eps;
+  hipEvent_t e1;
+  int rc;
+  for (int li = 0; li < c.num_layers; ++li) {
+    const Layer& L = h->layers[li];
+    if ((rc = gemm_f32<EPI_F32>(h, hs, L.fqkv, L.bqkv, nullptr, qkv, M, 3 * H, H, st))) return rc;
+    pbegin(h, h->p_attn, st, &e1);
+    hipLaunchKernelGGL(k_attention_f32, dim3((unsigned)(B * nh), (unsigned)((S + 127) / 128)), dim3(256), 0, st, qkv,
+                       d_mask, ctx, S, nh, H);
+    pend(h, h->p_attn, st, e1, 4.0 * B * nh * (double)S * S * HD);
+    BCHK(h, hipGetLastError());
+    if ((rc = gemm_f32<EPI_RESID_F32>(h, ctx, L.fo, L.bo, hs, tmp, M, H, H, st))) return rc;
+    if ((rc = layernorm(h, tmp, L.ln1w, L.ln1b, hs, nullptr, M, H, eps, st))) return rc;
+    if ((rc = gemm_f32<EPI_GELU_F32>(h, hs, L.fi, L.bi, nullptr, inter, M, I, H, st))) return rc;
+    if ((rc = gemm_f32<EPI_RESID_F32>(h, inter, L.fo2, L.bo2, hs, tmp, M, H, I, st))) return rc;
+    if ((rc = layernorm(h, tmp, L.ln2w, L.ln2b, hs, nullptr, M, H, eps, st))) return rc;
   }
-  float* hs = (float*)h->ws;
+  return FHE_OK;
+}
+
+// the bf16 forward (FHE_BERT_BF16): bf16 GEMM operands, f32 accumulation,
+// workspace h f32 | tmp f32 | hb bf16 | qkv bf16 | ctx bf16 | inter bf16
+static int forward_bf16(fhe_bert* h, const int32_t* d_mask, int B, int S, float* hs, hipStream_t st) {
+  const fhe_bert_config& c = h->cfg;
+  const int H = c.hidden_size, I = c.intermediate_size, nh = c.num_heads, M = B * S;
   float* tmp = hs + (size_t)M * H;
   bf16* hb = (bf16*)(tmp + (size_t)M * H);
   bf16* qkv = hb + (size_t)M * H;
   bf16* ctx = qkv + (size_t)M * 3 * H;
   bf16* inter = ctx + (size_t)M * H;
   const float eps = c.layer_norm_eps;
-  const unsigned rows4 = (unsigned)((M + 3) / 4);
-  hipEvent_t e1;
-  pbegin(h, h->p_other, st, &e1);
-  hipLaunchKernelGGL(k_embed_ln, dim3(rows4), dim3(256), 0, st, d_ids, d_type, h->we, h->pe, h->te, h->elnw, h->elnb,
-                     hs, hb, M, S, H, c.vocab_size, c.type_vocab_size, eps);
-  pend(h, h->p_other, st, e1, 0.0);
-  BCHK(h, hipGetLastError());
   const int Sp = (S + 63) / 64 * 64;
   const int anw = Sp <= 256 ? 8 : 4;  // waves per attention workgroup (k_attention)
   const size_t attn_lds = (size_t)Sp * KLD * 2 + (size_t)HD * (Sp + 8) * 2 + (size_t)anw * 16 * KLD * 2 + (size_t)Sp * 4;
-  static bool attn_attr = false;
-  if (!attn_attr) {
-    BCHK(h, hipFuncSetAttribute((const void*)k_attention<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    BCHK(h, hipFuncSetAttribute((const void*)k_attention<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attn_attr = true;
-  }
+  hipEvent_t e1;
   int rc;
   for (int li = 0; li < c.num_layers; ++li) {
     const Layer& L = h->layers[li];
@@ -749,22 +1046,56 @@ int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, c
     pend(h, h->p_attn, st, e1, 4.0 * B * nh * (double)S * S * HD);
     BCHK(h, hipGetLastError());
     if ((rc = gemm<EPI_RESID_F32>(h, ctx, L.wo, L.bo, hs, tmp, M, H, H, st))) return rc;
-    pbegin(h, h->p_other, st, &e1);
-    if (H % 256 == 0)
-      hipLaunchKernelGGL(k_layernorm4, dim3(rows4), dim3(256), 0, st, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps);
-    else
-      hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps);
-    pend(h, h->p_other, st, e1, 0.0);
+    if ((rc = layernorm(h, tmp, L.ln1w, L.ln1b, hs, hb, M, H, eps, st))) return rc;
     if ((rc = gemm<EPI_GELU_BF16>(h, hb, L.wi, L.bi, nullptr, inter, M, I, H, st))) return rc;
     if ((rc = gemm<EPI_RESID_F32>(h, inter, L.wo2, L.bo2, hs, tmp, M, H, I, st))) return rc;
-    pbegin(h, h->p_other, st, &e1);
-    if (H % 256 == 0)
-      hipLaunchKernelGGL(k_layernorm4, dim3(rows4), dim3(256), 0, st, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps);
-    else
-      hipLaunchKernelGGL(k_layernorm, dim3(rows4), dim3(256), 0, st, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps);
-    pend(h, h->p_other, st, e1, 0.0);
-    BCHK(h, hipGetLastError());
+    if ((rc = layernorm(h, tmp, L.ln2w, L.ln2b, hs, hb, M, H, eps, st))) return rc;
   }
+  return FHE_OK;
+}
+
+int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type, const int32_t* d_mask, int32_t B,
+                     int32_t S, int32_t pooling, float* d_out, void* stream) {
+  if (!h) return FHE_E_ARG;
+  const fhe_bert_config& c = h->cfg;
+  if (B < 0 || S < 1 || S > c.max_position || pooling < 0 || pooling > FHE_BERT_POOL_NONE ||
+      (B > 0 && (!d_ids || !d_mask || !d_out)))
+    return bfail(h, FHE_E_ARG, "bad forward arguments (1 <= S <= max_position)");
+  if (!fhe_bert_ready(h)) return bfail(h, FHE_E_STATE, "weights not loaded (fhe_bert_set_tensor)");
+  if (B == 0) return FHE_OK;
+  BCHK(h, hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int H = c.hidden_size, I = c.intermediate_size;
+  const int64_t M64 = (int64_t)B * S;
+  if (M64 > (1 << 24)) return bfail(h, FHE_E_ARG, "B * S too large: split the call");
+  const int M = (int)M64;
+  const bool f32 = h->precision == FHE_BERT_F32;
+  // workspace: h f32 | tmp f32 | hb bf16 | qkv bf16 | ctx bf16 | inter bf16,
+  // or (f32) h | tmp | qkv | ctx | inter, all f32
+  const size_t need = f32 ? (size_t)M * 4 * (H + H + 3 * H + H + I)
+                          : (size_t)M * (4 * H + 4 * H + 2 * H + 6 * H + 2 * H + 2 * I);
+  if (need > h->ws_bytes) {
+    if (h->ws) {
+      BCHK(h, hipDeviceSynchronize());
+      BCHK(h, hipFree(h->ws));
+      h->ws = nullptr;
+      h->ws_bytes = 0;
+    }
+    BCHK(h, hipMalloc(&h->ws, need));
+    h->ws_bytes = need;
+  }
+  float* hs = (float*)h->ws;
+  bf16* hb = (bf16*)(hs + 2 * (size_t)M * H);  // bf16: the GEMM copy of the embeddings' LayerNorm
+  const float eps = c.layer_norm_eps;
+  const unsigned rows4 = (unsigned)((M + 3) / 4);
+  hipEvent_t e1;
+  pbegin(h, h->p_other, st, &e1);
+  hipLaunchKernelGGL(k_embed_ln, dim3(rows4), dim3(256), 0, st, d_ids, d_type, h->we, h->pe, h->te, h->elnw, h->elnb,
+                     hs, f32 ? nullptr : hb, M, S, H, c.vocab_size, c.type_vocab_size, eps);
+  pend(h, h->p_other, st, e1, 0.0);
+  BCHK(h, hipGetLastError());
+  int rc;
+  if ((rc = f32 ? forward_f32(h, d_mask, B, S, hs, st) : forward_bf16(h, d_mask, B, S, hs, st))) return rc;
   if (pooling == FHE_BERT_POOL_NONE) {
     BCHK(h, hipMemcpyAsync(d_out, hs, (size_t)M * H * 4, hipMemcpyDeviceToDevice, st));
   } else {

@@ -36,6 +36,10 @@ struct ProfAcc {
   const char* kernel = nullptr;  // the last launched instantiation (rocprofv3's name)
 };
 
+struct fhe_ctx;
+static void prof_begin(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t* e1);
+static void prof_end(fhe_ctx* ctx, ProfAcc& a, hipStream_t st, hipEvent_t e1, int64_t items);
+
 struct fhe_ctx {
   fhe_params p{};
   int device = -1;
@@ -60,6 +64,7 @@ struct fhe_ctx {
   size_t ws_bytes = 0;
   bool prof = false;
   ProfAcc prof_br, prof_brf[4], prof_ks;  // blind rotation on the main / fast / fast2 / mid / mid2 gadget
+  ProfAcc prof_enc;                       // the fused client encryption + leveled dot (k_encrypt_linear)
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2
                        // (two waves per ciphertext; forced by FHEICP_BR_VARIANT=2), 3 (A/B builds)
   // A/B builds only (FHEICP_AB, tools/build_variant.sh): other v4 shapes
@@ -493,6 +498,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
     free_ev(ctx->prof_br);
     for (auto& a : ctx->prof_brf) free_ev(a);
     free_ev(ctx->prof_ks);
+    free_ev(ctx->prof_enc);
   }
   delete ctx;
 }
@@ -747,17 +753,57 @@ int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_
   return FHE_OK;
 }
 
+// GLWEs per pair of the packed feature encoding (k_client.h)
+static int packed_chunks(const fhe_params& p, int32_t D) { return (D + p.N - 1) / p.N; }
+
+int fhe_encrypt_packed_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
+                             uint64_t* d_glwe, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_glwe))) return fail(ctx, FHE_E_ARG, "bad packed-encrypt arguments");
+  if (B == 0) return FHE_OK;
+  const fhe_params& p = ctx->p;
+  const int G = packed_chunks(p, D);
+  if (B * G > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "packed-encrypt batch too large: split the call");
+  const ChaKey K = key_from_seed(seed);
+  const size_t lds = (size_t)p.k * p.N * 9;
+  hipLaunchKernelGGL(k_encrypt_packed, dim3((unsigned)(B * G)), dim3(256), lds, (hipStream_t)stream, K, p.N, p.k,
+                     p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, id0, d_glwe);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+int fhe_linear_packed_batch(fhe_ctx* ctx, const uint64_t* d_glwe, int64_t B, int32_t D, const int64_t* d_w,
+                            int64_t cst, uint64_t* d_out, void* stream) {
+  int rc = need_device(ctx);
+  if (rc) return rc;
+  if (B < 0 || D <= 0 || (B > 0 && (!d_glwe || !d_w || !d_out))) return fail(ctx, FHE_E_ARG, "bad packed-linear arguments");
+  if (B == 0) return FHE_OK;
+  if (B > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "packed-linear batch too large: split the call");
+  const fhe_params& p = ctx->p;
+  hipLaunchKernelGGL(k_linear_packed, dim3((unsigned)B), dim3(256), (size_t)p.k * p.N * 8, (hipStream_t)stream, p.N,
+                     p.k, d_glwe, (int)D, packed_chunks(p, D), d_w, ((u64)cst) << (64 - p.msg_bits), d_out);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
 int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
                              const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_out))) return fail(ctx, FHE_E_ARG, "bad encrypt-linear arguments");
   if (B == 0) return FHE_OK;
-  if (B > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "encrypt-linear batch too large: split the call");
   const fhe_params& p = ctx->p;
+  const int G = packed_chunks(p, D);
+  if (B > 0x7fffffffLL || B * G > 0x7fffffffffffLL) return fail(ctx, FHE_E_ARG, "encrypt-linear batch too large: split the call");
   const ChaKey K = key_from_seed(seed);
-  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, K, p.k * p.N, p.msg_bits,
-                     p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, d_w, ((u64)cst) << (64 - p.msg_bits), id0, d_out);
+  hipEvent_t e1;
+  prof_begin(ctx, ctx->prof_enc, (hipStream_t)stream, &e1);
+  ctx->prof_enc.kernel = "k_encrypt_linear";
+  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(256), (size_t)p.k * p.N * 8, (hipStream_t)stream, K, p.N,
+                     p.k, p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, d_w,
+                     ((u64)cst) << (64 - p.msg_bits), id0, d_out);
+  prof_end(ctx, ctx->prof_enc, (hipStream_t)stream, e1, B);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
@@ -1702,6 +1748,7 @@ static ProfAcc* prof_bucket(fhe_ctx* ctx, const char* kernel) {
   if (!strcmp(kernel, "blind_rotate_mid")) return &ctx->prof_brf[2];
   if (!strcmp(kernel, "blind_rotate_mid2")) return &ctx->prof_brf[3];
   if (!strcmp(kernel, "keyswitch")) return &ctx->prof_ks;
+  if (!strcmp(kernel, "encrypt_linear")) return &ctx->prof_enc;
   return nullptr;
 }
 

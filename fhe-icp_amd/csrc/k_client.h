@@ -154,54 +154,189 @@ __global__ void __launch_bounds__(256) k_encrypt(ChaKey K, int dim, int msg_bits
 }
 
 // ---- seeded (compressed) ciphertexts: the stored document corpus ----------
+// ---- packed features: the leveled circuit's inputs as GLWE messages --------
+//  The D features of pair b are the first coefficients of
+// G = ceil(D / N) GLWE messages M_g = sum_t x[b, gN + t] Delta X^t; GLWE g of
+// pair b has stream id id0 + b G + g: mask A_i[t] = word iN + t of
+// stream(TAG_ENC_MASK, id), noise E[t] = TUniform(word t of
+// stream(TAG_ENC_NOISE, id)), body B = sum_i A_i S_i + M + E mod X^N + 1.
+// The leveled dot product multiplies GLWE g by W_g = sum_t w[gN + t] X^-t and
+// sample-extracts coefficient 0 (sum_t w_t m_t), an LWE under the flattened
+// key (kN): with C_i = A_i W_g the extracted mask is a_{i,0} = C_i[0],
+// a_{i,u} = -C_i[N - u], i.e.
+//     a_{i,u} = sum_t w_t Ahat_i[t - u],  Ahat[m] = A[m] (m >= 0), -A[m + N] (m < 0),
+// and the body coefficient 0 of B W_g is sum_t w_t B[t]. One mask of kN words
+// per pair instead of one per feature: 16x fewer ChaCha20 blocks at D = 16.
+
+// acc[r] += sum_{t < Dg} w[t] Ahat[t - u0 - r] for r < 8: Ahat of one component
+// (A: N words in LDS), windows of 16 words slid by 8 features at a time (all
+// register indices static); features past Dg weigh 0.
+__device__ __forceinline__ u64 ahat(const u64* A, int m, int N) { return m >= 0 ? A[m] : (u64)0 - A[m + N]; }
+__device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const int64_t* __restrict__ w, int Dg,
+                                            u64 acc[8]) {
+  u64 win[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) win[q] = ahat(A, q - u0 - 7, N);
+  for (int j0 = 0; j0 < Dg; j0 += 8) {
+#pragma unroll
+    for (int q = 8; q < 16; ++q) {
+      const int m = j0 + q - u0 - 7;
+      win[q] = m < N ? ahat(A, m, N) : 0;  // m < N always while j0 + 7 < Dg <= N
+    }
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const u64 wj = j0 + jj < Dg ? (u64)w[j0 + jj] : 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] += wj * win[jj + 7 - r];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) win[q] = win[q + 8];
+  }
+}
+
+// Client side: GLWE encryption of the packed features (fhe_encrypt_packed_batch).
+// One 256-thread workgroup per GLWE (pair b, chunk g); the body's negacyclic
+// products with the binary key run as in k_keygen_bsk. glwe: [B][G][(k+1)N].
+__global__ void __launch_bounds__(256) k_encrypt_packed(ChaKey K, int N, int k, int msg_bits, int noise_bits,
+                                                        const u64* __restrict__ s_big, const int64_t* __restrict__ x,
+                                                        int D, int G, u64 id0, u64* __restrict__ glwe) {
+  extern __shared__ u64 shm[];
+  u64* A = shm;                                              // kN
+  unsigned char* S = reinterpret_cast<unsigned char*>(shm + (size_t)k * N);  // kN
+  const int64_t bg = blockIdx.x, b = bg / G;
+  const int g = (int)(bg - b * G), Dg = min(D - g * N, N);
+  const u64 id = id0 + (u64)bg;
+  u64* o = glwe + (size_t)bg * (k + 1) * N;
+  for (int blk = threadIdx.x; blk < k * N / 8; blk += 256) {
+    u64 m[8];
+    stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) A[8 * blk + q] = o[8 * blk + q] = m[q];
+  }
+  for (int t = threadIdx.x; t < k * N; t += 256) S[t] = (unsigned char)s_big[t];
+  __syncthreads();
+  const int per = N / 256, t0 = per * threadIdx.x;  // this thread's body coefficients [t0, t0 + per)
+  u64 body[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < k; ++i) {
+    const u64* Ai = A + (size_t)i * N;
+    for (int v = 0; v < N; ++v) {
+      if (!S[i * N + v]) continue;  // uniform across the workgroup
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < per) body[q] += ahat(Ai, t0 + q - v, N);
+    }
+  }
+  u64 e[8];
+  stream_block(K, TAG_ENC_NOISE, id, (uint32_t)(t0 >> 3), e);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (q >= per) break;
+    const int t = t0 + q;
+    const u64 msg = t < Dg ? (u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits) : 0;
+    o[(size_t)k * N + t] = body[q] + msg + (u64)tuniform(e[(t & 7)], noise_bits);
+  }
+}
+
+// The per-pair extraction shared by the two kernels below: thread t owns mask
+// words [8t, 8t + 8) of the output LWE (component i = 8t / N), with A of the
+// chunk in LDS. Returns nothing; accumulates into acc.
+__device__ __forceinline__ void packed_chunk_mask(const u64* A, int N, int k, const int64_t* __restrict__ wg, int Dg,
+                                                  u64 acc[8]) {
+  const int t8 = 8 * threadIdx.x;
+  if (t8 < k * N) {
+    const int i = t8 / N;
+    packed_mac8(A + (size_t)i * N, N, t8 - i * N, wg, Dg, acc);
+  }
+}
+
+// Server side: the leveled dot product over packed GLWE inputs
+// (fhe_linear_packed_batch): out[b] = sum_g Extract_0(GLWE_g W_g) +
+// trivial(cst Delta). One workgroup per pair, A of each chunk staged in LDS.
+__global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* __restrict__ glwe, int D, int G,
+                                                       const int64_t* __restrict__ w, u64 cst_scaled,
+                                                       u64* __restrict__ out) {
+  extern __shared__ u64 shm[];
+  __shared__ u64 red[4];
+  const int64_t b = blockIdx.x;
+  u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 bpart = 0;
+  for (int g = 0; g < G; ++g) {
+    const u64* in = glwe + ((size_t)b * G + g) * (k + 1) * N;
+    const int Dg = min(D - g * N, N);
+    __syncthreads();  // the previous chunk's readers are done
+    for (int t = threadIdx.x; t < k * N; t += 256) shm[t] = in[t];
+    for (int t = threadIdx.x; t < Dg; t += 256) bpart += (u64)w[g * N + t] * in[(size_t)k * N + t];
+    __syncthreads();
+    packed_chunk_mask(shm, N, k, w + g * N, Dg, acc);
+  }
+  const int t8 = 8 * threadIdx.x;
+  u64* o = out + (size_t)b * (k * N + 1);
+  if (t8 < k * N) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[t8 + q] = acc[q];
+  }
+  const u64 bs = block_sum_u64<256>(bpart, red);
+  if (threadIdx.x == 0) o[k * N] = bs + cst_scaled;
+}
+
+// Fused client encryption + leveled dot product (fhe_encrypt_linear_batch):
+// k_encrypt_packed then k_linear_packed without materialising the GLWEs. The
+// mask of each chunk is generated into LDS (one ChaCha20 block per thread),
+// the extracted mask accumulated in registers, and the body computed from it:
+// Extract_0(B W_g) = <a_g, s> + sum_t w_t (m_t + e_t) exactly (mod 2^64), so
+//   b = <a, s> + sum_j w_j (x_j Delta + e_j) + cst Delta,
+// bit-identical to the two kernels.
+__global__ void __launch_bounds__(256) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
+                                                        const u64* __restrict__ s_big, const int64_t* __restrict__ x,
+                                                        int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
+                                                        u64 id0, u64* __restrict__ out) {
+  extern __shared__ u64 shm[];
+  __shared__ u64 red[4];
+  const int64_t b = blockIdx.x;
+  u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 bpart = 0;
+  for (int g = 0; g < G; ++g) {
+    const u64 id = id0 + (u64)b * G + g;
+    const int Dg = min(D - g * N, N);
+    __syncthreads();  // the previous chunk's readers are done
+    for (int blk = threadIdx.x; blk < k * N / 8; blk += 256) {
+      u64 m[8];
+      stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
+    }
+    for (int blk = threadIdx.x; 8 * blk < Dg; blk += 256) {  // the features' noise words, 8 per block
+      u64 e[8];
+      stream_block(K, TAG_ENC_NOISE, id, (uint32_t)blk, e);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int t = 8 * blk + q;
+        if (t < Dg)
+          bpart += (u64)w[g * N + t] *
+                   (((u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits)) + (u64)tuniform(e[q], noise_bits));
+      }
+    }
+    __syncthreads();
+    packed_chunk_mask(shm, N, k, w + g * N, Dg, acc);
+  }
+  const int t8 = 8 * threadIdx.x;
+  u64* o = out + (size_t)b * (k * N + 1);
+  u64 sdot = 0;
+  if (t8 < k * N) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[t8 + q] = acc[q];
+      sdot += acc[q] & (0 - s_big[t8 + q]);
+    }
+  }
+  const u64 tot = block_sum_u64<256>(sdot + bpart, red);
+  if (threadIdx.x == 0) o[k * N] = tot + cst_scaled;
+}
+
 // A seeded LWE keeps only its body; the mask is stream(TAG_ENC_MASK, id) of
 // a PUBLIC mask key Km, the noise stream(TAG_ENC_NOISE, id) of a SECRET
 // noise key Kn. Document b of a corpus holds D bodies,
 // feature j under stream id id0[b] + j. 2049 -> 1 word per feature in HBM:
-// Fused fresh encryption + leveled dot product (fhe_encrypt_linear_batch):
-// out[b] = sum_j w[j] * Enc(x[b, j]) + trivial(cst) without materialising the
-// B x D input ciphertexts. Feature j of pair b is encrypted exactly as
-// k_encrypt would (mask stream (TAG_ENC_MASK, id0 + b*D + j), noise word 0 of
-// (TAG_ENC_NOISE, same id)); arithmetic mod 2^64 is linear, so the output is
-// bit-identical to k_encrypt followed by k_linear:
-//   mask = sum_j w_j a_j,  body = <mask, s> + sum_j w_j (e_j + x_j Delta) + cst.
-// One 256-thread workgroup per pair; thread t owns mask words [8t', 8t'+8)
-// for t' = t, t + 256, ...
-__global__ void __launch_bounds__(256) k_encrypt_linear(ChaKey K, int dim, int msg_bits, int noise_bits,
-                                                        const u64* __restrict__ s_big, const int64_t* __restrict__ x,
-                                                        int D, const int64_t* __restrict__ w, u64 cst_scaled,
-                                                        u64 id0, u64* __restrict__ out) {
-  __shared__ u64 red[4];
-  const int64_t b = blockIdx.x;
-  const u64 base = id0 + (u64)b * (u64)D;
-  u64* o = out + (size_t)b * (dim + 1);
-  u64 part = 0;
-  for (int blk = threadIdx.x; blk < dim / 8; blk += 256) {
-    u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < D; ++j) {
-      u64 m[8];
-      stream_block(K, TAG_ENC_MASK, base + (u64)j, (uint32_t)blk, m);
-      const u64 wj = (u64)w[j];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += wj * m[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      o[8 * blk + q] = acc[q];
-      part += acc[q] & (0 - s_big[8 * blk + q]);
-    }
-  }
-  const u64 sdot = block_sum_u64<256>(part, red);
-  // the body's per-feature terms, split over the workgroup
-  u64 bpart = 0;
-  for (int j = threadIdx.x; j < D; j += 256) {
-    const u64 e = (u64)tuniform(stream_word(K, TAG_ENC_NOISE, base + (u64)j, 0), noise_bits);
-    bpart += (u64)w[j] * (e + ((u64)x[(size_t)b * D + j] << (64 - msg_bits)));
-  }
-  const u64 bsum = block_sum_u64<256>(bpart, red);
-  if (threadIdx.x == 0) o[dim] = sdot + bsum + cst_scaled;
-}
-
 // the masks are regenerated where they are consumed (k_linear_seeded).
 __global__ void __launch_bounds__(256) k_encrypt_seeded(ChaKey Km, ChaKey Kn, int dim, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big,

@@ -60,6 +60,8 @@ SIGNATURES = [
     ("fhe_phase_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     ("fhe_encrypt_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _u64, _vp, _i64, _vp, _vp]),
+    ("fhe_encrypt_packed_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _u64, _vp, _vp]),
+    ("fhe_linear_packed_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     ("fhe_keyswitch_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
     ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
     ("fhe_pbs_gadget_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
@@ -98,6 +100,8 @@ SIGNATURES = [
     ("fhe_bert_create", C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p)]),
     ("fhe_bert_destroy", None, [_vp]),
     ("fhe_bert_last_error", C.c_char_p, [_vp]),
+    ("fhe_bert_set_precision", C.c_int, [_vp, _i32]),
+    ("fhe_bert_get_precision", C.c_int, [_vp]),
     ("fhe_bert_set_tensor", C.c_int, [_vp, _i32, _i32, _vp, _i64]),
     ("fhe_bert_ready", C.c_int, [_vp]),
     ("fhe_bert_forward", C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp]),

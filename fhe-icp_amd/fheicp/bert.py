@@ -1,13 +1,18 @@
 """The embedding stage's BERT encoder on the GPU.
 
 The reference runs ``transformers.AutoModel('bert-base-uncased')`` in torch
-(bert_embeddings.py:45, :136) and pools ``last_hidden_state`` on the host
-side of torch (:140-149). ``GpuBert`` takes the same model's weights (a
+fp32 (bert_embeddings.py:45, :136) and pools ``last_hidden_state`` on the
+host side of torch (:140-149). ``GpuBert`` takes the same model's weights (a
 ``transformers`` BertModel, or its state_dict + config) into libfheicp's
-encoder (include/fhe_bert.h: bf16 MFMA GEMMs, fused attention, fp32
-LayerNorm / residual / pooling) and returns the pooled embeddings on the
-device. There is no CPU fallback here: without libfheicp or a GPU the
-constructor raises.
+encoder (include/fhe_bert.h: MFMA GEMMs, fused attention, fp32 LayerNorm /
+residual / pooling) and returns the pooled embeddings on the device.
+
+``precision="f32"`` (default) is the reference's arithmetic: f32 operands on
+the f32 MFMA, torch's fp32 forward in another summation order.
+``precision="bf16"`` rounds the GEMM and attention operands to bf16 (about
+3x faster, looser agreement). ``provenance`` names the arithmetic for the
+stored-vector contract of batch_operations. There is no CPU
+fallback here: without libfheicp or a GPU the constructor raises.
 """
 from __future__ import annotations
 
@@ -20,6 +25,7 @@ from . import _lib
 from .engine import _ptr
 
 POOLING = {"mean": 0, "cls": 1, "max": 2, "none": 3}
+PRECISION = {"f32": 0, "bf16": 1}  # FHE_BERT_F32, FHE_BERT_BF16
 
 # HF state_dict name -> (layer or -1, tensor id of fhe_bert_set_tensor)
 _EMB = {"embeddings.word_embeddings.weight": 0, "embeddings.position_embeddings.weight": 1,
@@ -56,7 +62,9 @@ def _cfg_dict(config) -> dict:
 class GpuBert:
     """BERT forward + pooling on one MI355X through libfheicp (fhe_bert_*)."""
 
-    def __init__(self, model=None, state_dict=None, config=None, device: int = 0):
+    def __init__(self, model=None, state_dict=None, config=None, device: int = 0, precision: str = "f32"):
+        if precision not in PRECISION:
+            raise ValueError(f"precision must be one of {tuple(PRECISION)}")
         if not torch.cuda.is_available():
             raise _lib.FheError("GpuBert needs a ROCm GPU (torch.cuda.is_available() is False)")
         if model is not None:
@@ -73,6 +81,8 @@ class GpuBert:
         if rc != 0:
             raise _lib.FheError(f"fhe_bert_create failed ({_lib.ERRORS.get(rc, rc)}): unsupported config {self.cfg}")
         self._h = h
+        self._chk(self._L.fhe_bert_set_precision(self._h, PRECISION[precision]))
+        self.precision = precision
         prefix = "bert." if any(k.startswith("bert.") for k in state_dict) else ""
         for name, t in state_dict.items():
             key = name[len(prefix):] if prefix and name.startswith(prefix) else name
@@ -105,6 +115,11 @@ class GpuBert:
             self.close()
         except Exception:
             pass
+
+    @property
+    def provenance(self) -> str:
+        """The tag batch_operations stores with vectors this encoder embedded."""
+        return f"hip-bert-{self.precision}"
 
     @property
     def hidden_size(self) -> int:

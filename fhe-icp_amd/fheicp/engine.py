@@ -161,6 +161,27 @@ class Engine:
                                                    _ptr(wd), int(cst), _ptr(out), _stream(self.device)))
         return out
 
+    def encrypt_packed(self, msg, seed: int, id0: int = 0) -> torch.Tensor:
+        """Packed GLWE encryption of B x D features (fhe_encrypt_packed_batch):
+        [B][ceil(D / N)][(k + 1) N] words."""
+        m = self.to_dev(msg)
+        B, D = m.shape
+        p = self.params
+        G = -(-D // p.N)
+        out = torch.empty((B, G, (p.k + 1) * p.N), dtype=torch.int64, device=self.device)
+        self._chk(self._L.fhe_encrypt_packed_batch(self._ctx, _ptr(m), B, D, C.c_uint64(seed), C.c_uint64(id0),
+                                                   _ptr(out), _stream(self.device)))
+        return out
+
+    def linear_packed(self, glwe: torch.Tensor, D: int, w, cst: int) -> torch.Tensor:
+        """Leveled dot product on packed GLWE inputs (fhe_linear_packed_batch)."""
+        B = glwe.shape[0]
+        wd = self.to_dev(w)
+        out = self.empty_big(B)
+        self._chk(self._L.fhe_linear_packed_batch(self._ctx, _ptr(glwe), B, D, _ptr(wd), int(cst), _ptr(out),
+                                                  _stream(self.device)))
+        return out
+
     def keyswitch(self, ct: torch.Tensor, shift: int = 0, add_body: int = 0) -> torch.Tensor:
         n = ct.numel() // self.W
         out = self.empty_small(n)

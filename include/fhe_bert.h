@@ -1,7 +1,7 @@
 /*
  * fhe_bert.h — C ABI of the embedding stage's encoder in libfheicp.so
- * (SURVEY.md §8 f4): a BERT forward pass on gfx950 with bf16 MFMA GEMMs,
- * a fused flash-style attention kernel and fp32 LayerNorm / residual stream.
+ * (SURVEY.md §8 f4): a BERT forward pass on gfx950 (MFMA GEMMs, a fused
+ * flash-style attention kernel, fp32 LayerNorm / residual stream).
  *
  * Boundary. The reference embeds documents with
  * BertEmbedder.get_embedding / get_embeddings_batch
@@ -13,11 +13,20 @@
  * reference class). Weights are the transformers BertModel state_dict
  * (float32 host arrays, torch layout [out][in]), loaded once.
  *
- * Numerics: GEMM operands in bf16 (weights rounded once at load, activations
- * at each GEMM input), fp32 accumulation, fp32 bias / GELU (erf) / residual /
- * LayerNorm / softmax / pooling. Against the fp32 reference the pooled
- * embedding agrees to the tolerance tests/test_gpu_bert.py states; it is not
- * bit-equal (real-weight parity is unpinned: the weights are offline).
+ * Numerics (fhe_bert_set_precision):
+ *  - FHE_BERT_F32 (default): the reference's arithmetic. Every GEMM and both
+ *    attention products are f32 x f32 on v_mfma_f32_32x32x2_f32 (an exact f32
+ *    fma chain per output), f32 bias / GELU (library erff) / residual /
+ *    LayerNorm / softmax / pooling: torch's fp32 forward in another summation
+ *    order (tests/test_gpu_bert.py: hidden-state relative RMS <= 1e-5).
+ *  - FHE_BERT_BF16 (opt-in): GEMM and attention operands in bf16 (weights
+ *    rounded once at load, activations at each GEMM input), fp32
+ *    accumulation; ~3x faster, agreeing with the fp32 reference only to the
+ *    looser tolerance tests/test_gpu_bert.py states.
+ * Neither is bit-equal to torch (real-weight parity is unpinned: the weights
+ * are offline). A changed embedding can move a PCA feature across an input-
+ * quantizer rounding boundary, so the mirrors tag what this encoder embedded
+ * (DESIGN.md §7).
  *
  * Conventions as fhe_icp.h: 0 on success, negative FHE_E_* on failure,
  * fhe_bert_last_error for the message; d_* are device pointers; stream is a
@@ -60,12 +69,20 @@ enum {
 };
 /* pooling of fhe_bert_forward (bert_embeddings.py:140-149) */
 enum { FHE_BERT_POOL_MEAN = 0, FHE_BERT_POOL_CLS = 1, FHE_BERT_POOL_MAX = 2, FHE_BERT_POOL_NONE = 3 };
+/* arithmetic of the forward pass (see Numerics above) */
+enum { FHE_BERT_F32 = 0, FHE_BERT_BF16 = 1 };
 
+/* New handle on `device` (precision FHE_BERT_F32). */
 int fhe_bert_create(const fhe_bert_config* cfg, int device, fhe_bert** out);
+/* Select FHE_BERT_F32 or FHE_BERT_BF16; only before the first
+ * fhe_bert_set_tensor (FHE_E_STATE after: the weights are stored in the
+ * selected type). fhe_bert_get_precision returns the current one. */
+int fhe_bert_set_precision(fhe_bert* h, int32_t precision);
+int fhe_bert_get_precision(const fhe_bert* h);
 void fhe_bert_destroy(fhe_bert* h);
 const char* fhe_bert_last_error(const fhe_bert* h);
 /* Copy one float32 host tensor (count elements, torch layout) to the device,
- * converting GEMM weights to bf16; synchronous. */
+ * converting GEMM weights to bf16 under FHE_BERT_BF16; synchronous. */
 int fhe_bert_set_tensor(fhe_bert* h, int32_t layer, int32_t which, const float* h_data, int64_t count);
 /* 1 once every tensor of the config has been set */
 int fhe_bert_ready(const fhe_bert* h);
@@ -75,7 +92,8 @@ int fhe_bert_ready(const fhe_bert* h);
  * pooling MEAN / CLS / MAX writes d_out [B][hidden] float32 (mean over the
  * mask, row 0, max over all S positions, as bert_embeddings.py:140-149);
  * NONE writes last_hidden_state [B][S][hidden] float32. Workspace grows on
- * demand (~B*S*(hidden*10 + intermediate*2) bytes). */
+ * demand (B*S*(hidden*24 + intermediate*4) bytes under FHE_BERT_F32,
+ * B*S*(hidden*18 + intermediate*2) under FHE_BERT_BF16). */
 int fhe_bert_forward(fhe_bert* h, const int32_t* d_ids, const int32_t* d_type_ids, const int32_t* d_mask, int32_t B,
                      int32_t S, int32_t pooling, float* d_out, void* stream);
 /* Measurement: with profiling on, fhe_bert_forward brackets its kernel

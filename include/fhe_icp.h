@@ -146,12 +146,23 @@ int fhe_phase_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t count, uint64_t*
  * ct: B x D big ciphertexts (row-major), d_w: D int64 (device). */
 int fhe_linear_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                      uint64_t* d_out, void* stream);
-/* fhe_encrypt_batch of the B x D messages d_qx (ciphertext b*D + j uses
- * stream id id0 + b*D + j) followed by fhe_linear_batch, fused: the input
- * ciphertexts are never written (mod-2^64 linearity makes the output
- * bit-identical to the two calls). The single-party form of the reference's
- * predict(fhe="execute") (fhe_similarity.py:151): client encryption and the
- * server's leveled dot product in one pass; d_out: B x (kN+1). */
+/* Packed feature encryption, the client side of the
+ * reference's predict(fhe="execute") (fhe_similarity.py:151): the D features
+ * of row b (d_qx, B x D, encoded at Delta) are the first coefficients of
+ * G = ceil(D / N) GLWE messages; GLWE (b, g) uses stream id id0 + b*G + g.
+ * d_glwe: B x G x (k+1)N words [A_1 .. A_k, B] per GLWE. */
+int fhe_encrypt_packed_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
+                             uint64_t* d_glwe, void* stream);
+/* The leveled dot product on packed inputs (Concrete-ML
+ * LinearRegression._inference's q_x @ q_w + constant): out[b] = sum_g
+ * SampleExtract_0(GLWE(b, g) * sum_t d_w[gN + t] X^-t) + trivial(cst * Delta),
+ * a big LWE (B x (kN+1)) of sum_j d_w[j] x[b, j] + cst. Needs no secret key. */
+int fhe_linear_packed_batch(fhe_ctx* ctx, const uint64_t* d_glwe, int64_t B, int32_t D, const int64_t* d_w,
+                            int64_t cst, uint64_t* d_out, void* stream);
+/* fhe_encrypt_packed_batch followed by fhe_linear_packed_batch, fused: the
+ * GLWEs are never written (bit-identical to the two calls). The single-party
+ * form of predict(fhe="execute"): client encryption and the server's leveled
+ * dot product in one pass; d_out: B x (kN+1). */
 int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
                              const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream);
 /* big -> small key switch of (ct << shift) + add_body (shift/add used by the
@@ -325,7 +336,8 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
  * synchronises and returns total milliseconds, launch count and ciphertexts
  * processed for kernel "blind_rotate" (all gadgets), "blind_rotate_main",
  * "blind_rotate_fast" (fhe_params.pbs_fast_*), "blind_rotate_fast2",
- * "blind_rotate_mid", "blind_rotate_mid2" or "keyswitch", then resets what it
+ * "blind_rotate_mid", "blind_rotate_mid2", "keyswitch" or "encrypt_linear"
+ * (the fused client encryption + leveled dot), then resets what it
  * read. */
 int fhe_profile_enable(fhe_ctx* ctx, int enable);
 int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches, int64_t* items);

@@ -360,6 +360,83 @@ void ref_encrypt_ints(const ref_params* P, const uint64_t* s_big, const int64_t*
   free(m);
 }
 
+/* Packed features (GPU: k_encrypt_packed, k_linear_packed,
+ * k_encrypt_linear). The D features of row b fill the first coefficients of
+ * G = ceil(D / N) GLWE messages M_g = sum_t v[b][gN + t] Delta X^t; GLWE
+ * (b, g) has stream id id0 + b*G + g: A_i[t] = word iN + t of the TAG_ENC_MASK
+ * stream, E[t] = TUniform of word t of the TAG_ENC_NOISE stream, and the body
+ * B = sum_i A_i S_i + M + E (S_i: the GLWE secret's polynomials, s_big =
+ * S_1 .. S_k). Textbook: the body by full negacyclic products. glwe: B x G x
+ * (k+1)N words. */
+void ref_encrypt_packed(const ref_params* P, const uint64_t* s_big, const int64_t* v, int64_t B, int32_t D,
+                        uint64_t seed, uint64_t id0, uint64_t* glwe) {
+  ref_key K;
+  key_from_seed(seed, &K);
+  const int N = P->N, k = P->k, G = (D + N - 1) / N;
+#pragma omp parallel for schedule(dynamic)
+  for (int64_t bg = 0; bg < B * G; ++bg) {
+    const int64_t b = bg / G;
+    const int g = (int)(bg % G);
+    uint64_t* scratch = (uint64_t*)malloc(8 * (size_t)(16 * N));
+    ref_stream sm, sn;
+    stream_init(&sm, &K, TAG_ENC_MASK, id0 + (uint64_t)bg);
+    stream_init(&sn, &K, TAG_ENC_NOISE, id0 + (uint64_t)bg);
+    uint64_t* o = glwe + (size_t)bg * (k + 1) * N;
+    uint64_t* body = o + (size_t)k * N;
+    for (int t = 0; t < N; ++t) body[t] = 0;
+    for (int i = 0; i < k; ++i) {
+      for (int t = 0; t < N; ++t) o[(size_t)i * N + t] = stream_word(&sm, (uint64_t)i * N + t);
+      negacyclic_mac(o + (size_t)i * N, s_big + (size_t)i * N, body, N, scratch);
+    }
+    for (int t = 0; t < N; ++t) {
+      const int j = g * N + t;
+      const uint64_t m = j < D ? ((uint64_t)v[b * D + j]) << (64 - P->msg_bits) : 0;
+      body[t] += m + (uint64_t)tuniform(stream_word(&sn, (uint64_t)t), P->glwe_noise_bits);
+    }
+    free(scratch);
+  }
+}
+
+/* The leveled dot product on packed GLWEs: for each chunk, the GLWE times
+ * W_g = sum_t w[gN + t] X^-t (X^-t = -X^(N-t)), then the LWE of coefficient 0
+ * (sample extraction: a_{i,0} = C_i[0], a_{i,u} = -C_i[N-u], b = C_B[0]),
+ * summed over the chunks, plus trivial(cst * Delta). out: B x (kN+1). */
+void ref_linear_packed(const ref_params* P, const uint64_t* glwe, int64_t B, int32_t D, const int64_t* w, int64_t cst,
+                       uint64_t* out) {
+  const int N = P->N, k = P->k, G = (D + N - 1) / N, W = k * N + 1;
+#pragma omp parallel for schedule(dynamic)
+  for (int64_t b = 0; b < B; ++b) {
+    uint64_t* scratch = (uint64_t*)malloc(8 * (size_t)(16 * N));
+    uint64_t* wp = (uint64_t*)malloc(8 * (size_t)N);
+    uint64_t* c = (uint64_t*)malloc(8 * (size_t)N);
+    uint64_t* o = out + (size_t)b * W;
+    for (int t = 0; t < W; ++t) o[t] = 0;
+    for (int g = 0; g < G; ++g) {
+      const uint64_t* in = glwe + ((size_t)b * G + g) * (k + 1) * N;
+      for (int t = 0; t < N; ++t) wp[t] = 0;
+      for (int t = 0; t < N && g * N + t < D; ++t) {
+        const uint64_t wt = (uint64_t)w[g * N + t];
+        if (t == 0) wp[0] += wt;
+        else wp[N - t] -= wt;
+      }
+      for (int i = 0; i <= k; ++i) {
+        for (int t = 0; t < N; ++t) c[t] = 0;
+        negacyclic_mac(in + (size_t)i * N, wp, c, N, scratch);
+        if (i == k) {
+          o[k * N] += c[0];
+        } else {
+          o[(size_t)i * N] += c[0];
+          for (int u = 1; u < N; ++u) o[(size_t)i * N + u] -= c[N - u];
+        }
+      }
+    }
+    o[W - 1] += ((uint64_t)cst) << (64 - P->msg_bits);
+    free(scratch);
+    free(wp);
+    free(c);
+  }
+}
+
 /* Seeded encryption of a document corpus: feature j of
  * document b has stream id id0[b] + j; its mask is the TAG_ENC_MASK stream
  * of the public key `mkey`, its noise the TAG_ENC_NOISE stream of the

@@ -80,6 +80,8 @@ def lib():
         L.ref_tuniform.argtypes = [C.c_uint64, C.c_int]; L.ref_tuniform.restype = C.c_int64
         L.ref_chacha20_block.argtypes = [u32p, C.c_uint32, u32p, u32p]
         L.ref_encrypt_seeded.argtypes = [P, u64p, i64p, C.c_int64, C.c_int32, u32p, u32p, u64p, u64p]
+        L.ref_encrypt_packed.argtypes = [P, u64p, i64p, C.c_int64, C.c_int32, C.c_uint64, C.c_uint64, u64p]
+        L.ref_linear_packed.argtypes = [P, u64p, C.c_int64, C.c_int32, i64p, C.c_int64, u64p]
         L.ref_expand_seeded.argtypes = [P, u64p, u64p, C.c_int64, C.c_int32, u32p, u64p]
         L.ref_key_from_seed.argtypes = [C.c_uint64, u32p]
         _lib = L
@@ -141,6 +143,25 @@ class RefTFHE:
         ct = np.zeros((msg.size, self.big + 1), np.uint64)
         lib().ref_encrypt_raw(C.byref(self.P), u64(self.s_big), u64(msg), msg.size, seed, id0, u64(ct))
         return ct
+
+    def encrypt_packed(self, v, seed: int, id0: int = 0) -> np.ndarray:
+        """Packed GLWE encryption of B x D features: B x G x (k+1)N words."""
+        v = np.ascontiguousarray(v, dtype=np.int64)
+        B, D = v.shape
+        N, k = self.params["N"], self.params["k"]
+        G = -(-D // N)
+        glwe = np.zeros((B, G, (k + 1) * N), np.uint64)
+        lib().ref_encrypt_packed(C.byref(self.P), u64(self.s_big), i64(v), B, D, seed, id0, u64(glwe))
+        return glwe
+
+    def linear_packed(self, glwe: np.ndarray, D: int, w, cst: int) -> np.ndarray:
+        """Leveled dot product of packed GLWEs (sample extraction at 0)."""
+        glwe = np.ascontiguousarray(glwe, dtype=np.uint64)
+        B = glwe.shape[0]
+        w = np.ascontiguousarray(w, dtype=np.int64)
+        out = np.zeros((B, self.big + 1), np.uint64)
+        lib().ref_linear_packed(C.byref(self.P), u64(glwe), B, D, i64(w), cst, u64(out))
+        return out
 
     def encrypt_seeded(self, v, mask_key, noise_key, id0) -> np.ndarray:
         """Seeded corpus encryption (bodies only), v: B x D ints, id0: B stream ids."""

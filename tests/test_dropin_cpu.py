@@ -449,3 +449,64 @@ def test_gpu_reducer_contract_refuses_mixed_stores(tmp_path):
         g.compare_encrypted("a", "d")
     assert isinstance(mixed.compare_encrypted("a", "d"), float)
     assert g.compare_encrypted("a", "b") == pytest.approx(mixed.compare_encrypted("a", "b"))
+
+
+class _HipEmbedder(_Embedder):
+    """Stand-in for BertEmbedder(gpu_encoder=True) (its provenance tag)."""
+    provenance = "hip-bert-f32"
+
+
+def test_gpu_embedder_contract_refuses_mixed_stores(tmp_path):
+    """BatchConfig.gpu_embedder's contract, as the reducer's: documents the
+    HIP encoder embedded carry metadata[EMBEDDER_KEY] = its provenance, and
+    no score mixes them with torch-embedded vectors (search, compare, insert
+    raise unless allow_mixed_embedders)."""
+    from batch_operations import EMBEDDER_KEY, BatchConfig, BatchProcessor
+    from encrypted_storage import EncryptedDocumentStore
+    store = EncryptedDocumentStore(str(tmp_path))
+
+    def proc(hip, **kw):
+        c = BatchConfig(**{"fhe": "disable", "input_dim": 16, "n_bits": 6, "seed": 21, "show_progress": False,
+                           "key_manager_default": False, **kw})
+        return BatchProcessor(embedder=_HipEmbedder() if hip else _Embedder(), reducer=_Reducer(), storage=store,
+                              config=c)
+
+    g = proc(True)
+    g.encrypt_documents(["alpha doc", "beta doc"], doc_ids=["a", "b"])
+    assert all(store.index[i]["metadata"][EMBEDDER_KEY] == "hip-bert-f32" for i in "ab")
+    assert len(g.search_similar("alpha doc", top_k=2, min_similarity=-100)) == 2
+    cpu = proc(False)
+    with pytest.raises(ValueError, match="embedders"):
+        cpu.search_similar("alpha doc", top_k=2, min_similarity=-100)
+    with pytest.raises(ValueError, match="embedders"):
+        cpu.encrypt_documents(["delta doc"], doc_ids=["d"])
+    with pytest.raises(ValueError, match="embedders"):       # untagged vectors are the torch encoder's
+        g.store_vectors(np.zeros((1, 16), np.float32), ["v"])
+    g.store_vectors(np.zeros((1, 16), np.float32), ["v"], embedder="hip-bert-f32")
+    assert store.index["v"]["metadata"][EMBEDDER_KEY] == "hip-bert-f32"
+    mixed = proc(False, allow_mixed_embedders=True)
+    mixed.encrypt_documents(["delta doc"], doc_ids=["d"])
+    assert EMBEDDER_KEY not in store.index["d"]["metadata"]
+    with pytest.raises(ValueError, match="embedders"):
+        g.compare_encrypted("a", "d")
+    assert isinstance(mixed.compare_encrypted("a", "d"), float)
+    with pytest.raises(ValueError, match="gpu_embedder_precision"):
+        BatchConfig(gpu_embedder=True, gpu_embedder_precision="fp16")
+
+
+def test_store_vectors_tags_the_reducer(tmp_path):
+    """store_vectors takes the reducer of the config (GPU_REDUCER under
+    gpu_reducer) or an explicit one, tags it and runs the same check as
+    encrypt_documents."""
+    from batch_operations import GPU_REDUCER, REDUCER_KEY, BatchConfig, BatchProcessor
+    from encrypted_storage import EncryptedDocumentStore
+    store = EncryptedDocumentStore(str(tmp_path))
+    c = BatchConfig(fhe="disable", input_dim=16, n_bits=6, seed=21, show_progress=False, key_manager_default=False,
+                    gpu_reducer=True)
+    p = BatchProcessor(embedder=_Embedder(), reducer=_GpuTaggedReducer(), storage=store, config=c)
+    v = np.random.default_rng(1).standard_normal((3, 16)).astype(np.float32)
+    p.store_vectors(v[:2], ["x", "y"])
+    assert store.index["x"]["metadata"][REDUCER_KEY] == GPU_REDUCER
+    with pytest.raises(ValueError, match="reducers"):
+        p.store_vectors(v[2:], ["z"], reducer=None)
+    assert "z" not in store.index

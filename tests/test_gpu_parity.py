@@ -491,17 +491,26 @@ def test_threshold_batch_real(real):
 @pytest.mark.parametrize("which", ["toy", "real"])
 def test_encrypt_linear_fused_bit_exact(which, request):
     """fhe_encrypt_linear_batch (the fused client encryption + leveled dot of
-    fhe_compare_batch) is bit-identical to fhe_encrypt_batch followed by
-    fhe_linear_batch, and to the oracle's encrypt + linear, including a
-    feature count that is not a multiple of anything (D = 37)."""
+    fhe_compare_batch / fhe_score_batch, packed features: DESIGN.md §3.2) is
+    bit-identical to fhe_encrypt_packed_batch followed by
+    fhe_linear_packed_batch, and both to the oracle's textbook GLWE encryption
+    + product + sample extraction; GLWEs equal the oracle's word for word. D
+    covers a count that is not a multiple of anything (37), the compare
+    path's 16, and more features than N (two GLWEs per row)."""
     eng, ref = request.getfixturevalue(which)
     rng = np.random.default_rng(11)
-    for B, D in ((5, 37), (64, 16)):
+    N = eng.params.N
+    for B, D in ((5, 37), (64, 16), (3, N + 44)):
         x = rng.integers(-32, 32, (B, D))
         w = rng.integers(-127, 128, D)
         cst = int(rng.integers(-1000, 1000))
         fused = u64(eng.encrypt_linear(x, w, cst, seed=8, id0=77))
-        two = u64(eng.linear(eng.encrypt(x, seed=8, id0=77), B, D, w, cst))
-        assert np.array_equal(fused, two)
-        lin_ref = ref.linear(ref.encrypt_ints(x, seed=8, id0=77), B, D, w, cst)
-        assert np.array_equal(fused, lin_ref)
+        glwe = eng.encrypt_packed(x, seed=8, id0=77)
+        glwe_ref = ref.encrypt_packed(x, seed=8, id0=77)
+        assert np.array_equal(u64(glwe).reshape(glwe_ref.shape), glwe_ref), (B, D)
+        two = u64(eng.linear_packed(glwe, D, w, cst))
+        assert np.array_equal(fused, two), (B, D)
+        lin_ref = ref.linear_packed(glwe_ref, D, w, cst)
+        assert np.array_equal(fused, lin_ref), (B, D)
+        half = 2 ** (eng.msg_bits - 1)
+        assert np.array_equal(ref.decrypt_ints(lin_ref), (x @ w + cst + half) % (2 * half) - half)

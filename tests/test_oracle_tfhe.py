@@ -90,6 +90,63 @@ def test_encrypt_linear_decrypt(toy_ref):
     assert np.array_equal(toy_ref.decrypt_ints(lin), (x @ w + 3 + half) % (2 * half) - half)
 
 
+def _ahat_linear(glwe, D, w, cst, N, k, P):
+    """numpy restatement of the fused kernel's formulas (k_encrypt_linear /
+    k_linear_packed): a_{i,u} = sum_t w_t Ahat_i[t - u], Ahat[m] = A[m] (m >= 0),
+    -A[m + N] (m < 0); b = sum_t w_t B[t] + cst Delta; summed over chunks."""
+    B, G, _ = glwe.shape
+    out = np.zeros((B, k * N + 1), np.uint64)
+    u = np.arange(N)
+    with np.errstate(over="ignore"):
+        for g in range(G):
+            Dg = min(D - g * N, N)
+            for t in range(Dg):
+                wt = np.uint64(np.int64(w[g * N + t]) & np.int64(-1)) if w[g * N + t] >= 0 else \
+                    np.uint64(2 ** 64 + int(w[g * N + t]))
+                m = t - u
+                for i in range(k):
+                    A = glwe[:, g, i * N:(i + 1) * N]
+                    ah = np.where(m >= 0, A[:, m % N], np.uint64(0) - A[:, (m + N) % N])
+                    out[:, i * N:(i + 1) * N] += wt * ah
+                out[:, k * N] += wt * glwe[:, g, k * N + t]
+        out[:, k * N] += np.uint64((int(cst) << (64 - P)) % 2 ** 64)
+    return out
+
+
+@pytest.mark.parametrize("B,D", [(6, 8), (3, 300)])
+def test_packed_encrypt_linear(toy_ref, B, D):
+    """Packed features: the GLWE of a row decrypts
+    coefficient-wise to its features (the noise within TUniform's bound), the
+    textbook leveled product (GLWE x W, sample extraction) decrypts to
+    x @ w + cst, and equals the fused kernel's formulas restated in numpy bit
+    for bit, across a chunk boundary (D = 300 > N = 256: two GLWEs per row)."""
+    P = TOY.msg_bits
+    N, k = TOY.N, TOY.k
+    rng = np.random.default_rng(3)
+    x = rng.integers(-4, 4, (B, D))
+    w = rng.integers(-7, 8, D)
+    glwe = toy_ref.encrypt_packed(x, seed=9, id0=40)
+    G = -(-D // N)
+    assert glwe.shape == (B, G, (k + 1) * N)
+    from oracle.tfhe_ref import negacyclic_mul
+    S = toy_ref.s_big.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        for b in range(B):
+            for g in range(G):
+                ph = glwe[b, g, k * N:].copy()
+                for i in range(k):
+                    ph -= negacyclic_mul(glwe[b, g, i * N:(i + 1) * N], S[i * N:(i + 1) * N])
+                want = np.zeros(N, np.int64)
+                seg = x[b, g * N:(g + 1) * N]
+                want[:seg.size] = seg
+                err = ph.view(np.int64) - (want << (64 - P))
+                assert np.abs(err).max() <= 2 ** TOY.glwe_noise_bits
+    lin = toy_ref.linear_packed(glwe, D, w, 3)
+    half = 2 ** (P - 1)
+    assert np.array_equal(toy_ref.decrypt_ints(lin), (x @ w + 3 + half) % (2 * half) - half)
+    assert np.array_equal(lin, _ahat_linear(glwe, D, w, 3, N, k, P))
+
+
 def test_keyswitch_noise(toy_ref):
     rng = np.random.default_rng(2)
     v = rng.integers(-100, 100, 40)
