@@ -201,8 +201,11 @@ static void gemm3_launch(const bf16* A, const bf16* W, const float* bias, const 
 // per register group). Within a K step the MFMA's two k slots take the
 // halves of the 32-wide step (lane half h supplies k = 16 h + t at step t),
 // so a lane's operands are 64 contiguous bytes of one row: four b128 reads.
-constexpr int F_BK = 32, F_STAGE = (BM + G3_BN) * F_BK;  // floats per stage (48 KB)
-constexpr int F_LDS = 3 * F_STAGE * (int)sizeof(float);  // 147456 B
+constexpr int F_BK = 32;
+template <int FBN>
+constexpr int f_stage() { return (BM + FBN) * F_BK; }  // floats per stage (48 / 40 KB)
+template <int FBN>
+constexpr int f_lds() { return 3 * f_stage<FBN>() * (int)sizeof(float); }  // 147456 / 122880 B
 enum { EPI_F32 = 3, EPI_GELU_F32 = 4 };                   // (+ EPI_RESID_F32)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -210,12 +213,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // GELUActivation): the library erff, not the bf16 path's 1.5e-7 approximation
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
-template <int EPI>
+// FBN = 128 or 64 output columns per block (eight waves in 4 x 2, each 64 x
+// FBN/2); the host picks the one whose block count wastes the least of the
+// last wave of blocks (gemm3_f32_auto).
+template <int EPI, int FBN>
 __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, const float* __restrict__ W,
                                                    const float* __restrict__ bias, const float* __restrict__ resid,
                                                    float* __restrict__ out, int M, int N, int K, int tiles_n,
                                                    int nblk) {
-  constexpr int BN = G3_BN, WN = 2;  // 8 waves in 4 x 2, each 64 x 64
+  constexpr int WN = 2, NT = FBN / 64;  // 32-column MFMA tiles per wave
+  constexpr int STAGE = f_stage<FBN>(), WPIECES = FBN / 64;  // W pieces of 8 rows per wave and stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* st = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, l = tid & 63, h = l >> 5;
@@ -223,10 +230,10 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
   const int wm = w / WN, wn = w - wm * WN;
   const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
   const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * BN;
+  const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * FBN;
   const int KT = K / F_BK;
   auto issue = [&](int kt, int s) {
-    float* la = st + s * F_STAGE;
+    float* la = st + s * STAGE;
     float* lb = la + BM * F_BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // A: 32 pieces of 8 rows x 128 B, four per wave
@@ -236,16 +243,16 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
                                        0);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {  // W: 16 pieces, two per wave
-      const int pc = 2 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+    for (int i = 0; i < WPIECES; ++i) {  // W: FBN / 8 pieces
+      const int pc = WPIECES * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
       const int gn = min(n0 + row, N - 1);
       __builtin_amdgcn_global_load_lds(W + (size_t)gn * K + kt * F_BK + 4 * c, (lds_void*)(lb + pc * 8 * F_BK), 16, 0,
                                        0);
     }
   };
-  f32x16 acc[2][2];  // [n tile][m tile]
+  f32x16 acc[NT][2];  // [n tile][m tile]
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -253,44 +260,51 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
   issue(0, 0);
   if (KT > 1) issue(1, 1);
   for (int kt = 0; kt < KT; ++kt) {
-    if (kt + 1 < KT)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else
+    if (kt + 1 < KT) {
+      if constexpr (WPIECES == 2)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     if (kt + 2 < KT) issue(kt + 2, (kt + 2) % 3);
-    const float* la = st + (kt % 3) * F_STAGE;
+    const float* la = st + (kt % 3) * STAGE;
     const float* lb = la + BM * F_BK;
-    float4 wv[2][4], av[2][4];
+    float4 wv[NT][4], av[2][4];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int n = wn * 64 + 32 * j + (l & 31), m = wm * 64 + 32 * j + (l & 31);
+      const int m = wm * 64 + 32 * j + (l & 31);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        wv[j][u] = *reinterpret_cast<const float4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
-        av[j][u] = *reinterpret_cast<const float4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
-      }
+      for (int u = 0; u < 4; ++u) av[j][u] = *reinterpret_cast<const float4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = wn * (FBN / 2) + 32 * j + (l & 31);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wv[j][u] = *reinterpret_cast<const float4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < NT; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i][u][e], av[j][u][e], acc[i][j], 0, 0, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's reads retire before the next barrier
   }
-  // epilogue through LDS as k_gemm3: the wave's 64 x 64 tile row-major in a
-  // private region (pitch 68 floats), then whole 256-byte row pieces
+  // epilogue through LDS as k_gemm3: the wave's 64 x FBN/2 tile row-major in
+  // a private region (pitch FBN/2 + 4 floats), then whole row pieces
   __syncthreads();
-  const int colw = n0 + wn * 64, roww = m0 + wm * 64;
-  if (colw >= N) return;
-  constexpr int EPL = 68;
+  constexpr int WCOL = FBN / 2, EPL = WCOL + 4;
+  const int colw = n0 + wn * WCOL, roww = m0 + wm * 64;
+  if (colw >= N) return;  // N % 64 == 0: a wave's columns are all in or all out
   float* ep = reinterpret_cast<float*>(smem) + (size_t)w * (64 * EPL);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
       const int c = 32 * i + 8 * gq + 4 * h;  // four consecutive output columns of register group gq
@@ -307,9 +321,10 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
         *reinterpret_cast<float4*>(ep + rl * EPL + c) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
+  constexpr int CPR = WCOL / 4;  // 16-byte pieces per row
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int pc = l + 64 * it, rl = pc >> 4, cp = pc & 15;
+  for (int it = 0; it < 64 * CPR / 64; ++it) {
+    const int pc = l + 64 * it, rl = pc / CPR, cp = pc - rl * CPR;
     const int row = roww + rl;
     if (row >= M) continue;
     float4 v = *reinterpret_cast<const float4*>(ep + rl * EPL + 4 * cp);
@@ -322,12 +337,29 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
   }
 }
 
-template <int EPI>
+template <int EPI, int FBN>
 static void gemm3_f32_launch(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
                              int N, int K, hipStream_t st) {
-  const int tiles_n = (N + G3_BN - 1) / G3_BN, nblk = tiles_n * ((M + BM - 1) / BM);
-  hipLaunchKernelGGL(k_gemm3_f32<EPI>, dim3((unsigned)nblk), dim3(512), F_LDS, st, A, W, bias, resid, out, M, N, K,
-                     tiles_n, nblk);
+  const int tiles_n = (N + FBN - 1) / FBN, nblk = tiles_n * ((M + BM - 1) / BM);
+  hipLaunchKernelGGL((k_gemm3_f32<EPI, FBN>), dim3((unsigned)nblk), dim3(512), f_lds<FBN>(), st, A, W, bias, resid,
+                     out, M, N, K, tiles_n, nblk);
+}
+// 128 or 64 columns per block: the one whose last wave of blocks (one block
+// per CU, 256 CUs) is fuller, 128 unless 64 wastes clearly less
+static int f32_block_cols(int M, int N) {
+  auto waste = [&](int bn) {
+    const long tiles = (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM);
+    return (double)((tiles + 255) / 256 * 256) / (double)tiles;
+  };
+  return waste(64) < waste(128) - 0.03 ? 64 : 128;
+}
+template <int EPI>
+static void gemm3_f32_auto(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
+                           int N, int K, hipStream_t st) {
+  if (f32_block_cols(M, N) == 64)
+    gemm3_f32_launch<EPI, 64>(A, W, bias, resid, out, M, N, K, st);
+  else
+    gemm3_f32_launch<EPI, 128>(A, W, bias, resid, out, M, N, K, st);
 }
 
 // ---- fused attention (flash-style) ------------------------------------------
@@ -767,9 +799,12 @@ int fhe_bert_create(const fhe_bert_config* c, int device, fhe_bert** out) {
       hipFuncSetAttribute((const void*)k_gemm3<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
       hipFuncSetAttribute((const void*)k_gemm3<EPI_GELU_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
       hipFuncSetAttribute((const void*)k_gemm3<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_GELU_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<128>()) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_GELU_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<128>()) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_RESID_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<128>()) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_F32, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<64>()) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_GELU_F32, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<64>()) ||
+      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_RESID_F32, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<64>()) ||
       hipFuncSetAttribute((const void*)k_attention<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ||
       hipFuncSetAttribute((const void*)k_attention<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
     rc = FHE_E_DEVICE;
@@ -968,7 +1003,7 @@ static int gemm_f32(fhe_bert* h, const float* A, const float* W, const float* bi
                     int M, int N, int K, hipStream_t st) {
   hipEvent_t e1;
   pbegin(h, h->p_gemm, st, &e1);
-  gemm3_f32_launch<EPI>(A, W, bias, resid, out, M, N, K, st);
+  gemm3_f32_auto<EPI>(A, W, bias, resid, out, M, N, K, st);
   pend(h, h->p_gemm, st, e1, 2.0 * M * N * K);
   BCHK(h, hipGetLastError());
   return FHE_OK;

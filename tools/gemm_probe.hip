@@ -1,7 +1,7 @@
-// Probe of the BERT GEMM (fhe-icp_amd/csrc/bert.hip k_gemm3) at the embed
-// bench's shapes (25.6k tokens, random bf16 operands): HIP-event time per
-// launch and TFLOP/s. Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DFBERT_AB_NOEPI]
-//        tools/gemm_probe.hip -o gemm_probe
+// Probe of the BERT GEMMs (fhe-icp_amd/csrc/bert.hip k_gemm3, bf16, and
+// k_gemm3_f32, f32) at the embed bench's shapes (25.6k tokens, random
+// operands): HIP-event time per launch and TFLOP/s.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DFBERT_AB_NOEPI] tools/gemm_probe.hip -o gemm_probe
 #include "../fhe-icp_amd/csrc/bert.hip"
 
 #include <cstdio>
@@ -52,7 +52,53 @@ int main() {
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     ms /= 10;
-    printf("N=%d K=%d epi=%d: %.1f us, %.0f TF/s\n", N, K, epi, ms * 1e3, 2.0 * M * N * K / (ms * 1e-3) / 1e12);
+    printf("bf16 N=%d K=%d epi=%d: %.1f us, %.0f TF/s\n", N, K, epi, ms * 1e3, 2.0 * M * N * K / (ms * 1e-3) / 1e12);
+  }
+  // f32: the reference's arithmetic (EPI_F32 = QKV, EPI_GELU_F32 = FFN1, EPI_RESID_F32 = out / FFN2)
+  float *Af, *Wf;
+  hipMalloc(&Af, (size_t)M * 3072 * 4);
+  hipMalloc(&Wf, (size_t)3072 * 3072 * 4);
+  {
+    std::vector<float> h((size_t)M * 3072);
+    uint32_t x = 777;
+    for (auto& v : h) {
+      x = x * 1664525u + 1013904223u;
+      v = (float)((int)(x >> 8) - (1 << 23)) / (float)(1 << 23);
+    }
+    hipMemcpy(Af, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(Wf, h.data(), (size_t)3072 * 3072 * 4, hipMemcpyHostToDevice);
+  }
+  const int fshapes[4][3] = {{2304, 768, EPI_F32}, {768, 768, EPI_RESID_F32}, {3072, 768, EPI_GELU_F32},
+                             {768, 3072, EPI_RESID_F32}};
+#define FATTR(E, B) hipFuncSetAttribute((const void*)k_gemm3_f32<E, B>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<B>())
+  FATTR(EPI_F32, 128); FATTR(EPI_GELU_F32, 128); FATTR(EPI_RESID_F32, 128);
+  FATTR(EPI_F32, 64); FATTR(EPI_GELU_F32, 64); FATTR(EPI_RESID_F32, 64);
+  for (int bn : {128, 64}) {
+    for (auto& sh : fshapes) {
+      const int N = sh[0], K = sh[1], epi = sh[2];
+      float* o = (float*)out;
+      auto run = [&]() {
+        if (bn == 128) {
+          if (epi == EPI_F32) gemm3_f32_launch<EPI_F32, 128>(Af, Wf, bias, resid, o, M, N, K, 0);
+          else if (epi == EPI_GELU_F32) gemm3_f32_launch<EPI_GELU_F32, 128>(Af, Wf, bias, resid, o, M, N, K, 0);
+          else gemm3_f32_launch<EPI_RESID_F32, 128>(Af, Wf, bias, resid, o, M, N, K, 0);
+        } else {
+          if (epi == EPI_F32) gemm3_f32_launch<EPI_F32, 64>(Af, Wf, bias, resid, o, M, N, K, 0);
+          else if (epi == EPI_GELU_F32) gemm3_f32_launch<EPI_GELU_F32, 64>(Af, Wf, bias, resid, o, M, N, K, 0);
+          else gemm3_f32_launch<EPI_RESID_F32, 64>(Af, Wf, bias, resid, o, M, N, K, 0);
+        }
+      };
+      run();
+      hipEventRecord(e0, 0);
+      for (int r = 0; r < 10; ++r) run();
+      hipEventRecord(e1, 0);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      ms /= 10;
+      printf("f32 BN=%d N=%d K=%d epi=%d: %.1f us, %.1f TF/s (auto picks BN=%d)\n", bn, N, K, epi, ms * 1e3,
+             2.0 * M * N * K / (ms * 1e-3) / 1e12, f32_block_cols(M, N));
+    }
   }
   return 0;
 }
