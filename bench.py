@@ -534,6 +534,9 @@ def leveled_score(args, model, q_dev, d_dev, acc_compare) -> dict:
     avg_s = k["total_ms"] / max(k["launches"], 1) * 1e-3
     tops = ops / avg_s / 1e12 if k["launches"] else 0.0
     out_bytes = 8 * (p.k * p.N + 1) * B
+    # executed VALU instructions of this build (PMC, tools/pmc_bench.sh), x 64 lanes
+    pm = load_pmc().get(f"k_encrypt_linear@{B}", {})
+    pmc_ops = 64.0 * pm["valu_insts_per_launch"] if "valu_insts_per_launch" in pm else None
     return {"value": round(B * reps / el, 1), "unit": "scores/s", "ms_per_batch": round(el / reps * 1e3, 4),
             "acc_equal_to_compare": bool(torch.equal(acc, acc_compare)),
             "roofline": {"kernel": eng.kernel_name("encrypt_linear"), "bound": "valu-int",
@@ -542,6 +545,9 @@ def leveled_score(args, model, q_dev, d_dev, acc_compare) -> dict:
                          "launches": k["launches"], "pairs_per_launch": B,
                          "ops_per_pair": leveled_ops_per_pair(p, args.dim),
                          "ops_model": f"{CHACHA_BLOCK_OPS} per ChaCha20 block + {U64_MAC_OPS} per u64 MAC",
+                         "pmc_valu_lane_ops_per_launch": pmc_ops,
+                         "pmc_executed_frac": round(pmc_ops / avg_s / 1e12 / VALU_PEAK_TOPS, 4)
+                         if pmc_ops and k["launches"] else None,
                          "hbm": {"bytes_per_launch": out_bytes,
                                  "achieved_gbs": round(out_bytes / avg_s / 1e9, 1) if k["launches"] else 0.0,
                                  "peak_gbs": HBM_PEAK_GBS}}}

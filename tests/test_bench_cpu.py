@@ -70,3 +70,18 @@ def _port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def test_leveled_ops_model():
+    """bench.leveled_ops_per_pair (the k_encrypt_linear roofline's algorithmic
+    work): one kN-word GLWE mask per chunk of N features (kN / 8 ChaCha20
+    blocks), ceil(Dg / 8) noise blocks per chunk, D x kN u64 multiply-adds."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    from fheicp.params import params_for_bits
+    p = params_for_bits(16)
+    kN = p.k * p.N
+    assert bench.leveled_ops_per_pair(p, 16) == bench.CHACHA_BLOCK_OPS * (kN // 8 + 2) + bench.U64_MAC_OPS * kN * 16
+    # two chunks past N features (1100 = 1024 + 76): two masks, 128 + 10 noise blocks
+    assert bench.leveled_ops_per_pair(p, 1100) == (bench.CHACHA_BLOCK_OPS * (2 * kN // 8 + 128 + 10)
+                                                   + bench.U64_MAC_OPS * kN * 1100)

@@ -31,7 +31,7 @@ def kname(s: str) -> str:
     return s.split("(")[0]
 
 
-def per_kernel(path, match=("k_blind_rotate", "k_keyswitch")):
+def per_kernel(path, match=("k_blind_rotate", "k_keyswitch", "k_encrypt_linear")):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
         n = kname(r["Kernel_Name"])
