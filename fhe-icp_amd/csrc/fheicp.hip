@@ -236,7 +236,14 @@ static double ks_var(const fhe_params& p) {
   return (double)p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk +
          p.k * p.N / 2.0 * std::ldexp(1.0, -2 * p.ks_level * p.ks_base_log) / 12.0;
 }
-static double ms_var(const fhe_params& p) { return (p.n / 2.0 + 1) / 12.0 / ((2.0 * p.N) * (2.0 * p.N)); }
+// modulus switch to 2N: one rounding per set key bit and the body (classic);
+// the multi-bit rotation rounds the active subset's exponent from the exact
+// sum (k_blind_rotate.h mb_rotate), one rounding per pair with a set bit
+static double ms_var(const fhe_params& p, int group = 1) {
+  const double per = group == 2 ? (p.n / 2) * 0.75 / 12.0 + (p.n % 2) * 0.5 / 12.0 + 1.0 / 12.0
+                                : (p.n / 2.0 + 1) / 12.0;
+  return per / ((2.0 * p.N) * (2.0 * p.N));
+}
 
 // Decision margin in sigmas of the worst round of a d-bit digit sign
 // extraction on one gadget: the staircase round of the lowest digit, margin
@@ -268,10 +275,11 @@ static double plan_worst(const fhe_params& p, int d, const int* sched) {
   double var[NGAD];
   for (int g = 0; g < NGAD; ++g)
     var[g] = gadget_level(p, g) ? pbs_var(p, gadget_base_log(p, g), gadget_level(p, g), gadget_group(p, g)) : 0.0;
-  const double fixed = ks_var(p) + ms_var(p);
+  double fixed[NGAD];  // key switch + the modulus switch of each gadget's rotation
+  for (int g = 0; g < NGAD; ++g) fixed[g] = ks_var(p) + ms_var(p, gadget_group(p, g));
   double acc = 0, worst = 1e300;
   for (int r = 0; r < R; ++r) {
-    worst = std::min(worst, std::ldexp(1.0, ml[r]) / std::sqrt(acc * std::ldexp(1.0, 2 * sh[r]) + fixed));
+    worst = std::min(worst, std::ldexp(1.0, ml[r]) / std::sqrt(acc * std::ldexp(1.0, 2 * sh[r]) + fixed[sched[r]]));
     acc += var[sched[r]];
   }
   // the last bootstrap's output is the sign ciphertext: decryptable at 1/4

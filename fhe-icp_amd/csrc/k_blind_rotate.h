@@ -669,8 +669,11 @@ __global__ void __launch_bounds__(v4::nthreads(G), A32 ? 3 : 2) k_blind_rotate_v
 // bits (s1, s2); the key holds, per pair, GGSWs of the three indicators
 // m_S = [s1 s2 pattern = S] for S = {1}, {2}, {1,2} (k_mb_msgs). One step per
 // pair:
-//   ACC += ExtProd(ACC, sum_S (X^{a_S} - 1) GGSW(m_S)),  a_{1,2} = a1 + a2,
-// which rotates ACC by a1 s1 + a2 s2: exactly one m_S is 1 unless s1 = s2 = 0.
+//   ACC += ExtProd(ACC, sum_S (X^{a_S} - 1) GGSW(m_S)),
+// which rotates ACC by a_S of the one m_S that is 1 (none when s1 = s2 = 0).
+// Each exponent is switched to 2N from its exact sum: a_{1,2} = round((A1 +
+// A2) 2N / 2^64), not round(A1) + round(A2), so a pair with both bits set
+// adds one rounding error to the phase instead of two (ms_var).
 // The monomials act in the FFT domain: output position j of the forward
 // transform holds the evaluation at psi^{e_j}, psi = exp(i pi / N),
 // e_j = 4 bitrev9(j) + 1 (mb_exponent), so X^a multiplies it by psi^{a e_j}
@@ -755,7 +758,11 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   constexpr int G = 4, NT = nthreads(G), NPSI = 2 * N;
   constexpr int OFF_TW = NPSI, OFF_X = OFF_TW + NTW, NC64 = OFF_X + G * WPC * SCR;
   __shared__ c64 lds[NC64];
-  __shared__ uint32_t atab[mb::NP_MAX][G];  // a1 | a2 << 16 per pair and ciphertext
+  // per pair and ciphertext: a1 | e << 11 | a2 << 16, with e - 1 = a12 - a1 - a2
+  // (mod 2N) in {-1, 0, 1}: the pair's third exponent a12 is the switch of
+  // the exact sum of its two mask words (one rounding, not two, when both key
+  // bits are set: 3/4 of the pair's modulus-switch variance, ms_var)
+  __shared__ uint32_t atab[mb::NP_MAX][G];
   c64* psil = lds;
   c64* twl = lds + OFF_TW;
   c64* xbuf = lds + OFF_X;
@@ -788,13 +795,16 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   for (int x = tid; x < G * np; x += NT) {
     const int gg = x / np, jj = x - gg * np;
     const int64_t cc = (int64_t)blockIdx.x * G + gg;
-    uint32_t a1 = 0, a2 = 0;
+    uint32_t a1 = 0, a2 = 0, e = 1;
     if (cc < count) {
       const u64* sm = small + (size_t)cc * (n + 1);
       a1 = modswitch_2n(sm[2 * jj], 11);
-      if (2 * jj + 1 < n) a2 = modswitch_2n(sm[2 * jj + 1], 11);
+      if (2 * jj + 1 < n) {
+        a2 = modswitch_2n(sm[2 * jj + 1], 11);
+        e = (modswitch_2n(sm[2 * jj] + sm[2 * jj + 1], 11) - a1 - a2 + 1) & (2 * N - 1);  // 0, 1 or 2
+      }
     }
-    atab[jj][gg] = a1 | (a2 << 16);
+    atab[jj][gg] = a1 | (e << 11) | (a2 << 16);
   }
   __syncthreads();
   // this wave's product quarter: slots 2g, 2g+1; the exponent of slot 2g in
@@ -871,9 +881,9 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
       const uint32_t aa = __builtin_amdgcn_readfirstlane(atab[j][gg]);
-      aS[gg][0] = aa & 0xffffu;
+      aS[gg][0] = aa & 0x7ffu;
       aS[gg][1] = aa >> 16;
-      aS[gg][2] = (aS[gg][0] + aS[gg][1]) & (2 * N - 1);
+      aS[gg][2] = (aS[gg][0] + aS[gg][1] + ((aa >> 11) & 3u) - 1u) & (2 * N - 1);
     }
     c64 v[S];
     uint32_t dg[(L > 1 && A32) ? L - 1 : 1][S];

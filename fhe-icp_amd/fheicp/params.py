@@ -142,12 +142,14 @@ def _gadget_var(p: "SchemeParams", g: int) -> float:
 
 def _sched_worst(p: "SchemeParams", d: int, sched) -> float:
     """Worst decision margin (sigmas) when bootstrap r runs on gadget
-    sched[r] (fheicp.hip plan_worst)."""
+    sched[r] (fheicp.hip plan_worst); round r's modulus switch is that of its
+    own gadget's rotation (classic or multi-bit)."""
     vs = {g: _gadget_var(p, g) for g in set(sched)}
-    _, v_ks, v_ms = _variances(p)
+    vms = {g: _ms_var(p, gadget_of(p, g)[2]) for g in set(sched)}
+    _, v_ks, _ = _variances(p)
     acc, worst = 0.0, math.inf
     for r, (sh, ml) in enumerate(sign_rounds(p.msg_bits, d)):
-        worst = min(worst, 2.0 ** ml / math.sqrt(acc * 4.0 ** sh + v_ks + v_ms))
+        worst = min(worst, 2.0 ** ml / math.sqrt(acc * 4.0 ** sh + v_ks + vms[sched[r]]))
         acc += vs[sched[r]]
     # the last bootstrap's output is the sign ciphertext: decryptable at 1/4
     return min(worst, 0.25 / math.sqrt(vs[sched[-1]]))
@@ -370,8 +372,23 @@ def _variances(p: SchemeParams, group: int = 1):
     Bk = 2.0 ** p.ks_base_log
     v_ks = p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk
     v_ks += p.k * p.N / 2 * (2.0 ** (-2 * p.ks_level * p.ks_base_log)) / 12.0
-    v_ms = (p.n / 2 + 1) / 12.0 / (2.0 * p.N) ** 2
+    v_ms = _ms_var(p, group)
     return v_pbs, v_ks, v_ms
+
+
+def _ms_var(p: SchemeParams, group: int = 1) -> float:
+    """Modulus-switch variance of a bootstrap's input phase (relative to the
+    torus). Classic rotation: each of the ~n/2 set key bits and the body
+    carry one rounding to 1/(2N), 1/12 each. Multi-bit (group 2, DESIGN.md
+    §4.5): the rotation by sum_i a_i s_i uses the exponent of the ACTIVE
+    subset, rounded from the exact sum (round(a1 + a2) for s = (1, 1)), so a
+    pair carries one rounding if any bit is set: 3/4 x 1/12 per full pair,
+    1/2 x 1/12 for a lone last coefficient, plus the body's."""
+    if group == 2:
+        per = (p.n // 2) * 0.75 / 12.0 + (p.n % 2) * 0.5 / 12.0 + 1.0 / 12.0
+    else:
+        per = (p.n / 2 + 1) / 12.0
+    return per / (2.0 * p.N) ** 2
 
 
 def _digit_margin(p: SchemeParams, d: int) -> float:

@@ -627,7 +627,9 @@ static void add_rot_minus(const uint64_t* p, uint32_t a, int N, uint64_t* acc) {
 }
 
 /* Multi-bit blind rotation (group 2), exact: per pair j with
- * a1, a2 (a2 = 0 past n) and a12 = a1 + a2 mod 2N,
+ * a1, a2 (a2 = 0 past n) switched to 2N and a12 the switch of the exact sum
+ * of the two mask words (not a1 + a2: one rounding, not two, when both key
+ * bits are set),
  *   G_r = sum_S (X^{a_S} - 1) GGSW_S[r]   (exact, mod 2^64),
  *   ACC += sum_r digits_r(ACC) * G_r,
  * the algebra of k_blind_rotate_mb (the GPU forms the same products in the
@@ -641,7 +643,8 @@ static void pbs1_mb(const ref_params* P, const uint64_t* bsk, const uint64_t* sm
   for (int j = 0; j < npairs(P); ++j) {
     const uint32_t a1 = modswitch(small[2 * j], lg);
     const uint32_t a2 = 2 * j + 1 < n ? modswitch(small[2 * j + 1], lg) : 0;
-    const uint32_t aS[3] = {a1, a2, (a1 + a2) & (uint32_t)(2 * N - 1)};
+    const uint32_t a12 = 2 * j + 1 < n ? modswitch(small[2 * j] + small[2 * j + 1], lg) : a1;
+    const uint32_t aS[3] = {a1, a2, a12};
     if (!a1 && !a2) continue;
     for (size_t x = 0; x < ggsw; ++x) G[x] = 0;
     for (int S = 0; S < 3; ++S) {
@@ -889,13 +892,21 @@ static double pbs_variance(const ref_params* P, int base_log, int L, int group) 
   }
   return key + steps / (12.0 * pow(beta, 2.0 * L)) + steps * arith;
 }
-static double fixed_variance(const ref_params* P) {
+/* key switch + modulus switch of a bootstrap on a rotation of `group`: the
+ * classic one rounds every set key bit's exponent and the body's (1/12
+ * each); the multi-bit one (pbs1_mb) rounds the active subset's exponent
+ * from the exact sum, one rounding per pair with a set bit (3/4 of the full
+ * pairs, 1/2 of a lone last coefficient) */
+static double fixed_variance_g(const ref_params* P, int group) {
   const double bk = ldexp(1.0, P->ks_base_log);
   const double ks = (double)P->k * P->N * P->ks_level * (bk * bk + 2) / 12.0 * tu_var(P->lwe_noise_bits) /
                         ldexp(1.0, 128) +
                     P->k * P->N / 2.0 * ldexp(1.0, -2 * P->ks_level * P->ks_base_log) / 12.0;
-  return ks + (P->n / 2.0 + 1) / 12.0 / ((2.0 * P->N) * (2.0 * P->N));
+  const double per = group == 2 ? (P->n / 2) * 0.75 / 12.0 + (P->n % 2) * 0.5 / 12.0 + 1.0 / 12.0
+                                : (P->n / 2.0 + 1) / 12.0;
+  return ks + per / ((2.0 * P->N) * (2.0 * P->N));
 }
+static double fixed_variance(const ref_params* P) { return fixed_variance_g(P, 1); }
 /* rounds of the extraction in order: (shift, log2 margin); returns the count */
 static int plan_rounds(int Pb, int d, int* shift, int* mlog) {
   int R = 0, b = 0;
@@ -918,10 +929,11 @@ static double plan_margin(const ref_params* P, int d, const int* sched) {
   double var[NGAD];
   for (int g = 0; g < NGAD; ++g)
     var[g] = gadget_level(P, g) ? pbs_variance(P, gadget_base_log(P, g), gadget_level(P, g), gadget_group(P, g)) : 0.0;
-  const double fx = fixed_variance(P);
+  double fx[NGAD];
+  for (int g = 0; g < NGAD; ++g) fx[g] = fixed_variance_g(P, gadget_group(P, g));
   double acc = 0, worst = INFINITY;
   for (int r = 0; r < R; ++r) {
-    const double m = ldexp(1.0, ml[r]) / sqrt(acc * ldexp(1.0, 2 * sh[r]) + fx);
+    const double m = ldexp(1.0, ml[r]) / sqrt(acc * ldexp(1.0, 2 * sh[r]) + fx[sched[r]]);
     if (m < worst) worst = m;
     acc += var[sched[r]];
   }

@@ -80,8 +80,11 @@ def test_fast_gadget_plan():
     and every round keeps 9.2 sigma with the fewest main, then fast, rounds."""
     from fheicp.params import _plan_worst, plan_cost
     F, F2 = (15, 2, 2), (23, 1, 2)
-    want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F, F2, (4, 0, 1)), 12: (F, F2, (4, 0, 1)),
-            13: (F, F2, (4, 0, 3)), 16: (F, F2, (4, 0, 3))}
+    # (round 4: the multi-bit rounds' modulus switch rounds each pair's active
+    # exponent once, 3/4 of the classic variance, so P = 9 now runs on (23,1)
+    # alone and P = 13 needs two (15,2) rounds instead of three)
+    want = {4: (F2, None, (4, 0, 1)), 8: (F2, None, (4, 0, 3)), 9: (F2, None, (4, 0, 4)), 12: (F, F2, (4, 0, 1)),
+            13: (F, F2, (4, 0, 2)), 16: (F, F2, (4, 0, 3))}
     for P, (fg, fg2, (d, j1, j2)) in want.items():
         p = params_for_bits(P)
         assert p.pbs_mid_level == 0, P
@@ -117,8 +120,8 @@ def test_mid_gadget_plan():
     from dataclasses import replace
     from fheicp.params import _sched_worst, plan_cost, sign_schedule
     M3, M4, M5, M6 = (12, 3, 2), (10, 4, 2), (8, 5, 2), (7, 6, 2)
-    want = {17: (M3, None), 19: (M3, None), 20: (M4, M3), 21: (M4, M3), 22: (M5, M3), 23: (M5, M4),
-            24: (M4, M3), 25: (M5, M3), 26: (M5, M3), 27: (M6, M4)}
+    want = {17: (M3, None), 19: (M3, None), 20: (M4, None), 21: (M4, M3), 22: (M5, M3), 23: (M5, M3),
+            24: (M6, M4), 25: (M4, M3), 26: (M5, M3), 27: (M6, M4)}
     for P, (m1, m2) in want.items():
         p = params_for_bits(P)
         assert (p.pbs_mid_base_log, p.pbs_mid_level, p.pbs_mid_group) == m1, P
@@ -139,11 +142,12 @@ def test_mid_gadget_plan():
         assert plan_cost(p) < plan_cost(nomid), P
         classic = replace(p, pbs_mid_group=0, pbs_mid2_group=0)
         assert plan_cost(p) < plan_cost(classic), P
-    # C5's width: 1 main (5,8) classic, 2 mid (8,5) and 2 mid2 (12,3) multi-bit,
+    # C5's width: 1 main (6,7) classic ((5,8) before the multi-bit rounds'
+    # single rounding per pair), 2 mid (8,5) and 2 mid2 (12,3) multi-bit,
     # 4 fast, 4 fast2
     p26 = params_for_bits(26)
     assert (p26.pbs_base_log, p26.pbs_level, p26.pbs_mid_base_log, p26.pbs_mid_level,
-            p26.pbs_mid2_base_log, p26.pbs_mid2_level) == (5, 8, 8, 5, 12, 3)
+            p26.pbs_mid2_base_log, p26.pbs_mid2_level) == (6, 7, 8, 5, 12, 3)
     assert sign_schedule(p26)[1] == [0, 3, 3, 4, 4] + [1] * 4 + [2] * 4
     # the headline width runs every round on the multi-bit fast gadgets: the
     # main (15, 2) key is made but never launched
@@ -151,11 +155,50 @@ def test_mid_gadget_plan():
     # the headline width has no mid gadget; C3's (P = 21) takes the (10,4)
     # gadget, whose quieter first bootstrap allows 4-bit digits (10 bootstraps
     # instead of 13), on the multi-bit rotation for its first round (the
-    # classic (10,4) main key is made, never launched), then 2 x mb (12,3)
+    # classic (10,4) main key is made, never launched), then 2 x mb (12,3),
+    # 3 x mb (15,2) and 4 x mb (23,1) (4 and 3 before round 4)
     assert params_for_bits(16).pbs_mid_level == 0
     p21 = params_for_bits(21)
     assert (p21.pbs_base_log, p21.pbs_level) == (10, 4)
-    assert sign_schedule(p21) == (4, [3, 4, 4, 1, 1, 1, 1, 2, 2, 2])
+    assert sign_schedule(p21) == (4, [3, 4, 4, 1, 1, 1, 2, 2, 2, 2])
+
+
+def test_multibit_modswitch_variance():
+    """The multi-bit modulus switch (DESIGN.md §4.5, pbs1_mb / mb_rotate): the
+    phase error of a rotation by the active subset's exponent, each exponent
+    switched from its exact sum, simulated over random masks and binary keys
+    at the real n = 887, 2N = 2048: its variance matches params._ms_var
+    (group 2, 3/4 of the classic one per pair) within 3%, and the classic
+    per-coefficient rounding matches group 1."""
+    from fheicp.params import _ms_var, params_for_bits
+    p = params_for_bits(16)
+    rng = np.random.default_rng(5)
+    T, n, twoN = 4000, p.n, 2 * p.N
+    A = rng.integers(0, 2 ** 63, (T, n + 1), dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, (T, n + 1)).astype(np.uint64)
+    s = rng.integers(0, 2, (T, n)).astype(np.int64)
+
+    def sw(x):  # round(x 2N / 2^64) mod 2N, and the rounding error in units of the torus
+        r = ((x >> np.uint64(52)) + np.uint64(1)) >> np.uint64(1)
+        err = (r.astype(np.float64) - x.astype(np.float64) * twoN / 2.0 ** 64)
+        return r % twoN, (err + twoN / 2) % twoN - twoN / 2
+
+    _, eb = sw(A[:, n])
+    _, e = sw(A[:, :n])
+    classic = eb - (e * s).sum(1)
+    m = n // 2
+    a1, a2 = A[:, 0:2 * m:2], A[:, 1:2 * m:2]
+    s1, s2 = s[:, 0:2 * m:2], s[:, 1:2 * m:2]
+    _, e1 = sw(a1)
+    _, e2 = sw(a2)
+    with np.errstate(over="ignore"):
+        _, e12 = sw(a1 + a2)
+    pair = np.where((s1 == 1) & (s2 == 1), e12, np.where(s1 == 1, e1, np.where(s2 == 1, e2, 0.0)))
+    lone = e[:, n - 1] * s[:, n - 1] if n % 2 else 0.0
+    mb = eb - pair.sum(1) - lone
+    v1, v2 = classic.var() / twoN ** 2, mb.var() / twoN ** 2
+    assert abs(v1 / _ms_var(p, 1) - 1) < 0.05, v1 / _ms_var(p, 1)
+    assert abs(v2 / _ms_var(p, 2) - 1) < 0.05, v2 / _ms_var(p, 2)
+    assert 0.7 < _ms_var(p, 2) / _ms_var(p, 1) < 0.8
 
 
 def test_multibit_noise_model():
@@ -169,9 +212,9 @@ def test_multibit_noise_model():
         v1, v2 = _variances(p)[0], _variances(p, group=2)[0]
         assert 1.05 < v2 / v1 < 1.8, (b, lv, v2 / v1)
     # a plan whose fast gadget flips to classic when the group changes differs
-    q = params_for_bits(17)
+    q = params_for_bits(20)
     assert q.pbs_fast_group == 2 and q.pbs_fast2_group == 2
-    assert sign_plan(replace(q, pbs_fast_group=1, pbs_fast2_group=1)) != sign_plan(q)
+    assert sign_schedule(replace(q, pbs_fast_group=1, pbs_fast2_group=1))[1] != sign_schedule(q)[1]
 
 
 def test_sign_digit_bits_validation():
