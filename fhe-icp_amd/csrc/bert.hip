@@ -272,18 +272,21 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
     if (kt + 2 < KT) issue(kt + 2, (kt + 2) % 3);
     const float* la = st + (kt % 3) * STAGE;
     const float* lb = la + BM * F_BK;
-    float4 wv[NT][4], av[2][4];
+    // f32x4 (an ext_vector), not HIP's float4 struct: with the struct's loads
+    // hipcc waited vmcnt(0) before the first ds_read of every K step, i.e.
+    // for the DMA of step kt + 2 just issued (the pipeline drained each step)
+    f32x4 wv[NT][4], av[2][4];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int m = wm * 64 + 32 * j + (l & 31);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) av[j][u] = *reinterpret_cast<const float4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
+      for (int u = 0; u < 4; ++u) av[j][u] = *reinterpret_cast<const f32x4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = wn * (FBN / 2) + 32 * j + (l & 31);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wv[j][u] = *reinterpret_cast<const float4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
+      for (int u = 0; u < 4; ++u) wv[j][u] = *reinterpret_cast<const f32x4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)

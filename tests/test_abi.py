@@ -260,3 +260,20 @@ def test_wide_multibit_and_ks_coin_bounds():
         P = _lib.params_struct(ok)
         assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0 and h.value
         L.fhe_ctx_destroy(h)
+
+
+def test_gemm_lds_dma_pipelines_not_drained():
+    """ISA lint (no GPU): every BERT GEMM instantiation keeps its LDS-DMA
+    pipeline: no vmcnt(0) between the next step's global_load_lds and the
+    current step's first ds_read (tools/isa_lint.py)."""
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+    if not shutil.which("hipcc"):
+        pytest.skip("no hipcc")
+    repo = Path(__file__).resolve().parents[1]
+    r = subprocess.run([sys.executable, str(repo / "tools" / "isa_lint.py")], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert r.stdout.count("k_gemm3") >= 9
