@@ -272,31 +272,45 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
     if (kt + 2 < KT) issue(kt + 2, (kt + 2) % 3);
     const float* la = st + (kt % 3) * STAGE;
     const float* lb = la + BM * F_BK;
-    // f32x4 (an ext_vector), not HIP's float4 struct: with the struct's loads
-    // hipcc waited vmcnt(0) before the first ds_read of every K step, i.e.
-    // for the DMA of step kt + 2 just issued (the pipeline drained each step)
-    f32x4 wv[NT][4], av[2][4];
+    // Fragments as f32x4 (an ext_vector), not HIP's float4 struct: with the
+    // struct's loads hipcc waited vmcnt(0) before the first ds_read of every
+    // K step, i.e. for the DMA of step kt + 2 just issued (the pipeline
+    // drained each step). Group u (k = 16 h + 4 u .. + 3) is read one group
+    // ahead into the other register set; the scheduling barrier keeps those
+    // reads ahead of group u's MFMAs (left alone, hipcc reused one register
+    // set: read, wait, eight MFMAs, read ... with the LDS latency exposed)
+    f32x4 wv[2][NT], av[2][2];
+    auto rd = [&](int u, int bsel) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = wm * 64 + 32 * j + (l & 31);
+      for (int j = 0; j < 2; ++j) {
+        const int m = wm * 64 + 32 * j + (l & 31);
+        av[bsel][j] = *reinterpret_cast<const f32x4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
+      }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) av[j][u] = *reinterpret_cast<const f32x4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
-    }
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn * (FBN / 2) + 32 * j + (l & 31);
+        wv[bsel][j] = *reinterpret_cast<const f32x4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
+      }
+    };
+    rd(0, 0);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = wn * (FBN / 2) + 32 * j + (l & 31);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) wv[j][u] = *reinterpret_cast<const f32x4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 4; ++u) {
+      // group u's first MFMA (its wait covers group u's reads only), then
+      // group u + 1's reads, then the rest of group u
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[u & 1][0][0], av[u & 1][0][0], acc[0][0], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (u < 3) rd(u + 1, (u + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int i = 0; i < NT; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i][u][e], av[j][u][e], acc[i][j], 0, 0, 0);
+            if (e | i | j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[u & 1][i][e], av[u & 1][j][e], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's reads retire before the next barrier
   }
   // epilogue through LDS as k_gemm3: the wave's 64 x FBN/2 tile row-major in

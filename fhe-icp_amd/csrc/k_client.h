@@ -281,17 +281,21 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 
 // Fused client encryption + leveled dot product (fhe_encrypt_linear_batch):
 // k_encrypt_packed then k_linear_packed without materialising the GLWEs. The
-// mask of each chunk is generated into LDS (one ChaCha20 block per thread),
-// the extracted mask accumulated in registers, and the body computed from it:
-// Extract_0(B W_g) = <a_g, s> + sum_t w_t (m_t + e_t) exactly (mod 2^64), so
+// mask of each chunk is generated into LDS (one ChaCha20 block per thread of
+// waves 0-3), the extracted mask accumulated in registers, and the body
+// computed from it: Extract_0(B W_g) = <a_g, s> + sum_t w_t (m_t + e_t)
+// exactly (mod 2^64), so
 //   b = <a, s> + sum_j w_j (x_j Delta + e_j) + cst Delta,
-// bit-identical to the two kernels.
-__global__ void __launch_bounds__(256) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
+// bit-identical to the two kernels. The features' noise blocks go to a fifth
+// wave: on a mask thread, the two of D = 16 made its wave three blocks long
+// against one for the rest (27 us per 1024 pairs, 0.18 of the VALU roof).
+constexpr int EL_THREADS = 320;
+__global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big, const int64_t* __restrict__ x,
                                                         int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
                                                         u64 id0, u64* __restrict__ out) {
   extern __shared__ u64 shm[];
-  __shared__ u64 red[4];
+  __shared__ u64 red[EL_THREADS / 64];
   const int64_t b = blockIdx.x;
   u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 bpart = 0;
@@ -299,13 +303,14 @@ __global__ void __launch_bounds__(256) k_encrypt_linear(ChaKey K, int N, int k, 
     const u64 id = id0 + (u64)b * G + g;
     const int Dg = min(D - g * N, N);
     __syncthreads();  // the previous chunk's readers are done
-    for (int blk = threadIdx.x; blk < k * N / 8; blk += 256) {
+    for (int blk = threadIdx.x; blk < k * N / 8 && threadIdx.x < 256; blk += 256) {
       u64 m[8];
       stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
 #pragma unroll
       for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
     }
-    for (int blk = threadIdx.x; 8 * blk < Dg; blk += 256) {  // the features' noise words, 8 per block
+    // the features' noise words, 8 per block, on wave 4
+    for (int blk = (int)threadIdx.x - 256; blk >= 0 && 8 * blk < Dg; blk += EL_THREADS - 256) {
       u64 e[8];
       stream_block(K, TAG_ENC_NOISE, id, (uint32_t)blk, e);
 #pragma unroll
@@ -329,7 +334,7 @@ __global__ void __launch_bounds__(256) k_encrypt_linear(ChaKey K, int N, int k, 
       sdot += acc[q] & (0 - s_big[t8 + q]);
     }
   }
-  const u64 tot = block_sum_u64<256>(sdot + bpart, red);
+  const u64 tot = block_sum_u64<EL_THREADS>(sdot + bpart, red);
   if (threadIdx.x == 0) o[k * N] = tot + cst_scaled;
 }
 
