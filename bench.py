@@ -890,6 +890,24 @@ def embed_main(args, world, rank, local, dev):
                    "tolerance": f"cosine >= {tol['cos']}, max |diff| <= {tol['max']} (tests/test_gpu_bert.py)",
                    "within_tolerance": cos >= tol["cos"] and mxd <= tol["max"]},
     }
+    # the reference's own forward on this GPU (torch fp32 -> hipBLASLt / MIOpen,
+    # bert_embeddings.py:136 with device="cuda"), same batch, after the timed
+    # region: the yardstick of the HIP encoder in the same arithmetic
+    import copy
+    mg = copy.deepcopy(m).to(dev)
+    with torch.no_grad():
+        ids_g, mask_g = ids.to(dev), mask.to(dev)
+        mg(input_ids=ids_g, attention_mask=mask_g)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(max(args.steps, 2)):
+            mg(input_ids=ids_g, attention_mask=mask_g).last_hidden_state.mean(1)
+        torch.cuda.synchronize()
+        tg = (time.perf_counter() - t0) / max(args.steps, 2)
+    out_line["torch_gpu_fp32"] = {"value": round(B / tg, 2), "unit": "sequences/s", "ms_per_step": round(tg * 1e3, 3),
+                                  "what": "transformers BertModel fp32 forward + mean on this GPU (the reference's "
+                                          "BertEmbedder with device='cuda'), same batch"}
+    del mg
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = torch.get_num_threads()
         nb = 8

@@ -172,20 +172,29 @@ __global__ void __launch_bounds__(256) k_encrypt(ChaKey K, int dim, int msg_bits
 // (A: N words in LDS), windows of 16 words slid by 8 features at a time (all
 // register indices static); features past Dg weigh 0.
 __device__ __forceinline__ u64 ahat(const u64* A, int m, int N) { return m >= 0 ? A[m] : (u64)0 - A[m + N]; }
+// branch-free Ahat[m] for m in [-N, 2N), 0 from m = N on (features past the
+// chunk): one LDS read at m mod N and selects (the branchy form above made
+// every read its own divergent block, with its latency exposed)
+__device__ __forceinline__ u64 ahat_w(const u64* A, int m, int N) {
+  const u64 v = A[m & (N - 1)];
+  const u64 r = m < 0 ? (u64)0 - v : v;
+  return m < N ? r : 0;
+}
 __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const int64_t* __restrict__ w, int Dg,
                                             u64 acc[8]) {
   u64 win[16];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) win[q] = ahat(A, q - u0 - 7, N);
+  for (int q = 0; q < 8; ++q) win[q] = ahat_w(A, q - u0 - 7, N);
   for (int j0 = 0; j0 < Dg; j0 += 8) {
 #pragma unroll
-    for (int q = 8; q < 16; ++q) {
-      const int m = j0 + q - u0 - 7;
-      win[q] = m < N ? ahat(A, m, N) : 0;  // m < N always while j0 + 7 < Dg <= N
-    }
+    for (int q = 8; q < 16; ++q) win[q] = ahat_w(A, j0 + q - u0 - 7, N);
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const u64 wj = j0 + jj < Dg ? (u64)w[j0 + jj] : 0;
+      // the weight of feature j0 + jj (0 past Dg), read at a clamped index
+      // (wave-uniform: one scalar load)
+      const int j = j0 + jj;
+      const u64 wl = (u64)w[j < Dg ? j : Dg - 1];
+      const u64 wj = j < Dg ? wl : 0;
 #pragma unroll
       for (int r = 0; r < 8; ++r) acc[r] += wj * win[jj + 7 - r];
     }
