@@ -354,6 +354,132 @@ __global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, 
   }
 }
 
+// The same f32 GEMM on 128 x 128 blocks of four waves (2 x 2, each 64 x 64)
+// with two LDS stages (64 KB; the epilogue's 68 KB bound the allocation), so
+// two blocks share a CU and one's barriers and epilogue overlap the other's
+// MFMAs; a block re-reads a 128-row band of A, half the 256-row form's.
+constexpr int F2_BM = 128, F2_BN = 128, F2_STAGE = (F2_BM + F2_BN) * F_BK;
+constexpr int F2_LDS = 4 * 64 * 68 * (int)sizeof(float);  // epilogue 69632 B >= 2 stages (65536 B)
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) k_gemm2_f32(const float* __restrict__ A, const float* __restrict__ W,
+                                                      const float* __restrict__ bias, const float* __restrict__ resid,
+                                                      float* __restrict__ out, int M, int N, int K, int tiles_n,
+                                                      int nblk) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* st = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, l = tid & 63, h = l >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int m0 = (t / tiles_n) * F2_BM, n0 = (t - (t / tiles_n) * tiles_n) * F2_BN;
+  const int KT = K / F_BK;
+  auto issue = [&](int kt, int s) {
+    float* la = st + s * F2_STAGE;
+    float* lb = la + F2_BM * F_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // A: 16 pieces of 8 rows x 128 B, four per wave
+      const int pc = 4 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+      const int gm = min(m0 + row, M - 1);
+      __builtin_amdgcn_global_load_lds(A + (size_t)gm * K + kt * F_BK + 4 * c, (lds_void*)(la + pc * 8 * F_BK), 16, 0,
+                                       0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // W: 16 pieces, four per wave
+      const int pc = 4 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
+      const int gn = min(n0 + row, N - 1);
+      __builtin_amdgcn_global_load_lds(W + (size_t)gn * K + kt * F_BK + 4 * c, (lds_void*)(lb + pc * 8 * F_BK), 16, 0,
+                                       0);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  issue(0, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of stage kt
+    __builtin_amdgcn_s_barrier();                     // everyone's, and stage kt - 1 fully read
+    if (kt + 1 < KT) issue(kt + 1, (kt + 1) & 1);
+    const float* la = st + (kt & 1) * F2_STAGE;
+    const float* lb = la + F2_BM * F_BK;
+    f32x4 wv[2][2], av[2][2];
+    auto rd = [&](int u, int bsel) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = wm * 64 + 32 * j + (l & 31);
+        av[bsel][j] = *reinterpret_cast<const f32x4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
+        const int n = wn * 64 + 32 * j + (l & 31);
+        wv[bsel][j] = *reinterpret_cast<const f32x4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[u & 1][0][0], av[u & 1][0][0], acc[0][0], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (u < 3) rd(u + 1, (u + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            if (e | i | j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[u & 1][i][e], av[u & 1][j][e], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int colw = n0 + wn * 64, roww = m0 + wm * 64;
+  if (colw >= N) return;
+  constexpr int EPL = 68;
+  float* ep = reinterpret_cast<float*>(smem) + (size_t)w * (64 * EPL);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int c = 32 * i + 8 * gq + 4 * h;
+      const float4 bv4 = *reinterpret_cast<const float4*>(bias + colw + c);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rl = 32 * j + (l & 31);
+        float v[4] = {acc[i][j][4 * gq] + bv4.x, acc[i][j][4 * gq + 1] + bv4.y, acc[i][j][4 * gq + 2] + bv4.z,
+                      acc[i][j][4 * gq + 3] + bv4.w};
+        if constexpr (EPI == EPI_GELU_F32) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) v[rr] = gelu_erf(v[rr]);
+        }
+        *reinterpret_cast<float4*>(ep + rl * EPL + c) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int pc = l + 64 * it, rl = pc >> 4, cp = pc & 15;
+    const int row = roww + rl;
+    if (row >= M) continue;
+    float4 v = *reinterpret_cast<const float4*>(ep + rl * EPL + 4 * cp);
+    const size_t o = (size_t)row * N + colw + 4 * cp;
+    if constexpr (EPI == EPI_RESID_F32) {
+      const float4 rs = *reinterpret_cast<const float4*>(resid + o);
+      v = make_float4(v.x + rs.x, v.y + rs.y, v.z + rs.z, v.w + rs.w);
+    }
+    *reinterpret_cast<float4*>(out + o) = v;
+  }
+}
+template <int EPI>
+static void gemm2_f32_launch(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
+                             int N, int K, hipStream_t st) {
+  const int tiles_n = (N + F2_BN - 1) / F2_BN, nblk = tiles_n * ((M + F2_BM - 1) / F2_BM);
+  hipLaunchKernelGGL(k_gemm2_f32<EPI>, dim3((unsigned)nblk), dim3(256), F2_LDS, st, A, W, bias, resid, out, M, N, K,
+                     tiles_n, nblk);
+}
+
 template <int EPI, int FBN>
 static void gemm3_f32_launch(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
                              int N, int K, hipStream_t st) {

@@ -100,5 +100,27 @@ int main() {
              2.0 * M * N * K / (ms * 1e-3) / 1e12, f32_block_cols(M, N));
     }
   }
+  hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+  hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_GELU_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+  hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+  for (auto& sh : fshapes) {
+    const int N = sh[0], K = sh[1], epi = sh[2];
+    float* o = (float*)out;
+    auto run = [&]() {
+      if (epi == EPI_F32) gemm2_f32_launch<EPI_F32>(Af, Wf, bias, resid, o, M, N, K, 0);
+      else if (epi == EPI_GELU_F32) gemm2_f32_launch<EPI_GELU_F32>(Af, Wf, bias, resid, o, M, N, K, 0);
+      else gemm2_f32_launch<EPI_RESID_F32>(Af, Wf, bias, resid, o, M, N, K, 0);
+    };
+    run();
+    hipEventRecord(e0, 0);
+    for (int r = 0; r < 10; ++r) run();
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    ms /= 10;
+    printf("f32 k_gemm2 128x128x2wg N=%d K=%d epi=%d: %.1f us, %.1f TF/s\n", N, K, epi, ms * 1e3,
+           2.0 * M * N * K / (ms * 1e-3) / 1e12);
+  }
   return 0;
 }

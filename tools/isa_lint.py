@@ -14,7 +14,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 
 
-def gemm_drains(asm: str, pattern: str = "k_gemm3"):
+def gemm_drains(asm: str, pattern: str = "k_gemm"):
     out = {}
     for m in re.finditer(r"^(_Z\S*):\s*;", asm, re.M):
         nm = m.group(1)
