@@ -645,7 +645,7 @@ static void pbs1_mb(const ref_params* P, const uint64_t* bsk, const uint64_t* sm
     const uint32_t a2 = 2 * j + 1 < n ? modswitch(small[2 * j + 1], lg) : 0;
     const uint32_t a12 = 2 * j + 1 < n ? modswitch(small[2 * j] + small[2 * j + 1], lg) : a1;
     const uint32_t aS[3] = {a1, a2, a12};
-    if (!a1 && !a2) continue;
+    if (!a1 && !a2 && !a12) continue;  /* a12 can be +-1 with a1 = a2 = 0 */
     for (size_t x = 0; x < ggsw; ++x) G[x] = 0;
     for (int S = 0; S < 3; ++S) {
       if (!aS[S]) continue;
