@@ -191,173 +191,35 @@ static void gemm3_launch(const bf16* A, const bf16* W, const float* bias, const 
 }
 
 // ---- GEMM in the reference's arithmetic: f32 operands, f32 MFMA ----------
-// The same block structure with fp32 A and W: v_mfma_f32_32x32x2_f32 is an
-// exact f32 fma chain (one rounding per product, f32 accumulation), i.e. the
-// arithmetic of torch's fp32 Linear, in another summation order. K step 32
-// keeps the 128-byte rows of the bf16 kernel (eight 16-byte chunks, the same
-// XOR swizzle and LDS-DMA pieces), so the staging is byte-for-byte the one
-// above. Each wave owns 64 x 64 outputs as 2 x 2 tiles of 32 x 32; W is the
-// MFMA's A operand (D = W . A^T: a lane holds four consecutive output columns
-// per register group). Within a K step the MFMA's two k slots take the
-// halves of the 32-wide step (lane half h supplies k = 16 h + t at step t),
-// so a lane's operands are 64 contiguous bytes of one row: four b128 reads.
+// v_mfma_f32_32x32x2_f32 is an exact f32 fma chain (one rounding per
+// product, f32 accumulation), i.e. the arithmetic of torch's fp32 Linear in
+// another summation order. The K step is 32 floats, so a row of a stage is
+// the 128 bytes of the bf16 kernel's (eight 16-byte chunks, the same XOR
+// swizzle and LDS-DMA pieces). W is the MFMA's A operand (D = W . A^T: a lane
+// holds four consecutive output columns per register group); within a K step
+// the MFMA's two k slots take the halves of the step (lane half h supplies
+// k = 16 h + t at step t), so a lane's operands of a group are one b128 read
+// per 32-row tile.
 constexpr int F_BK = 32;
-template <int FBN>
-constexpr int f_stage() { return (BM + FBN) * F_BK; }  // floats per stage (48 / 40 KB)
-template <int FBN>
-constexpr int f_lds() { return 3 * f_stage<FBN>() * (int)sizeof(float); }  // 147456 / 122880 B
-enum { EPI_F32 = 3, EPI_GELU_F32 = 4 };                   // (+ EPI_RESID_F32)
+enum { EPI_F32 = 3, EPI_GELU_F32 = 4 };  // (+ EPI_RESID_F32)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // BERT's exact GELU in f32 (x * 0.5 * (1 + erf(x / sqrt(2))), transformers'
 // GELUActivation): the library erff, not the bf16 path's 1.5e-7 approximation
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
-// FBN = 128 or 64 output columns per block (eight waves in 4 x 2, each 64 x
-// FBN/2); the host picks the one whose block count wastes the least of the
-// last wave of blocks (gemm3_f32_auto).
-template <int EPI, int FBN>
-__global__ void __launch_bounds__(512) k_gemm3_f32(const float* __restrict__ A, const float* __restrict__ W,
-                                                   const float* __restrict__ bias, const float* __restrict__ resid,
-                                                   float* __restrict__ out, int M, int N, int K, int tiles_n,
-                                                   int nblk) {
-  constexpr int WN = 2, NT = FBN / 64;  // 32-column MFMA tiles per wave
-  constexpr int STAGE = f_stage<FBN>(), WPIECES = FBN / 64;  // W pieces of 8 rows per wave and stage
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* st = reinterpret_cast<float*>(smem);
-  const int tid = threadIdx.x, l = tid & 63, h = l >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WN, wn = w - wm * WN;
-  const int b = blockIdx.x, xcd = b & 7, q = nblk >> 3, r = nblk & 7;
-  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  const int m0 = (t / tiles_n) * BM, n0 = (t - (t / tiles_n) * tiles_n) * FBN;
-  const int KT = K / F_BK;
-  auto issue = [&](int kt, int s) {
-    float* la = st + s * STAGE;
-    float* lb = la + BM * F_BK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // A: 32 pieces of 8 rows x 128 B, four per wave
-      const int pc = 4 * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
-      const int gm = min(m0 + row, M - 1);  // rows past M: loaded, never stored
-      __builtin_amdgcn_global_load_lds(A + (size_t)gm * K + kt * F_BK + 4 * c, (lds_void*)(la + pc * 8 * F_BK), 16, 0,
-                                       0);
-    }
-#pragma unroll
-    for (int i = 0; i < WPIECES; ++i) {  // W: FBN / 8 pieces
-      const int pc = WPIECES * w + i, row = 8 * pc + (l >> 3), c = (l & 7) ^ (row & 7);
-      const int gn = min(n0 + row, N - 1);
-      __builtin_amdgcn_global_load_lds(W + (size_t)gn * K + kt * F_BK + 4 * c, (lds_void*)(lb + pc * 8 * F_BK), 16, 0,
-                                       0);
-    }
-  };
-  f32x16 acc[NT][2];  // [n tile][m tile]
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  issue(0, 0);
-  if (KT > 1) issue(1, 1);
-  for (int kt = 0; kt < KT; ++kt) {
-    if (kt + 1 < KT) {
-      if constexpr (WPIECES == 2)
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < KT) issue(kt + 2, (kt + 2) % 3);
-    const float* la = st + (kt % 3) * STAGE;
-    const float* lb = la + BM * F_BK;
-    // Fragments as f32x4 (an ext_vector), not HIP's float4 struct: with the
-    // struct's loads hipcc waited vmcnt(0) before the first ds_read of every
-    // K step, i.e. for the DMA of step kt + 2 just issued (the pipeline
-    // drained each step). Group u (k = 16 h + 4 u .. + 3) is read one group
-    // ahead into the other register set; the scheduling barrier keeps those
-    // reads ahead of group u's MFMAs (left alone, hipcc reused one register
-    // set: read, wait, eight MFMAs, read ... with the LDS latency exposed)
-    f32x4 wv[2][NT], av[2][2];
-    auto rd = [&](int u, int bsel) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int m = wm * 64 + 32 * j + (l & 31);
-        av[bsel][j] = *reinterpret_cast<const f32x4*>(la + m * F_BK + 4 * ((4 * h + u) ^ (m & 7)));
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = wn * (FBN / 2) + 32 * j + (l & 31);
-        wv[bsel][j] = *reinterpret_cast<const f32x4*>(lb + n * F_BK + 4 * ((4 * h + u) ^ (n & 7)));
-      }
-    };
-    rd(0, 0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      // group u's first MFMA (its wait covers group u's reads only), then
-      // group u + 1's reads, then the rest of group u
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[u & 1][0][0], av[u & 1][0][0], acc[0][0], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (u < 3) rd(u + 1, (u + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            if (e | i | j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[u & 1][i][e], av[u & 1][j][e], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's reads retire before the next barrier
-  }
-  // epilogue through LDS as k_gemm3: the wave's 64 x FBN/2 tile row-major in
-  // a private region (pitch FBN/2 + 4 floats), then whole row pieces
-  __syncthreads();
-  constexpr int WCOL = FBN / 2, EPL = WCOL + 4;
-  const int colw = n0 + wn * WCOL, roww = m0 + wm * 64;
-  if (colw >= N) return;  // N % 64 == 0: a wave's columns are all in or all out
-  float* ep = reinterpret_cast<float*>(smem) + (size_t)w * (64 * EPL);
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const int c = 32 * i + 8 * gq + 4 * h;  // four consecutive output columns of register group gq
-      const float4 bv4 = *reinterpret_cast<const float4*>(bias + colw + c);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int rl = 32 * j + (l & 31);
-        float v[4] = {acc[i][j][4 * gq] + bv4.x, acc[i][j][4 * gq + 1] + bv4.y, acc[i][j][4 * gq + 2] + bv4.z,
-                      acc[i][j][4 * gq + 3] + bv4.w};
-        if constexpr (EPI == EPI_GELU_F32) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) v[rr] = gelu_erf(v[rr]);
-        }
-        *reinterpret_cast<float4*>(ep + rl * EPL + c) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    }
-  constexpr int CPR = WCOL / 4;  // 16-byte pieces per row
-#pragma unroll
-  for (int it = 0; it < 64 * CPR / 64; ++it) {
-    const int pc = l + 64 * it, rl = pc / CPR, cp = pc - rl * CPR;
-    const int row = roww + rl;
-    if (row >= M) continue;
-    float4 v = *reinterpret_cast<const float4*>(ep + rl * EPL + 4 * cp);
-    const size_t o = (size_t)row * N + colw + 4 * cp;
-    if constexpr (EPI == EPI_RESID_F32) {
-      const float4 rs = *reinterpret_cast<const float4*>(resid + o);
-      v = make_float4(v.x + rs.x, v.y + rs.y, v.z + rs.z, v.w + rs.w);
-    }
-    *reinterpret_cast<float4*>(out + o) = v;
-  }
-}
-
-// The same f32 GEMM on 128 x 128 blocks of four waves (2 x 2, each 64 x 64)
-// with two LDS stages (64 KB; the epilogue's 68 KB bound the allocation), so
-// two blocks share a CU and one's barriers and epilogue overlap the other's
-// MFMAs; a block re-reads a 128-row band of A, half the 256-row form's.
+// 128 x 128 blocks of four waves (2 x 2, each 64 x 64 as 2 x 2 tiles of
+// 32 x 32) with two LDS stages (64 KB; the epilogue's 68 KB bound the
+// allocation), so two blocks share a CU and one's barriers and epilogue
+// overlap the other's MFMAs. Against the bf16 kernel's 256 x 128 blocks of
+// eight waves with three stages, in f32 (tools/gemm_probe.hip, docs/
+// AB_LOG_r04.md): +7-8% on all four encoder shapes (121.7 / 116.6 / 120.6 /
+// 123.0 TF against 113.5 / 108.4 / 111.4 / 114.4 at its best column width).
+// Group u (k = 16 h + 4 u .. + 3) is read one group ahead into the other
+// register set, behind group u's first MFMA (that MFMA's wait then covers
+// group u's reads only); fragments are f32x4 ext_vectors: with HIP's float4
+// struct hipcc waited vmcnt(0) before the first ds_read of every K step (the
+// DMA just issued), draining the pipeline (tools/isa_lint.py checks).
 constexpr int F2_BM = 128, F2_BN = 128, F2_STAGE = (F2_BM + F2_BN) * F_BK;
 constexpr int F2_LDS = 4 * 64 * 68 * (int)sizeof(float);  // epilogue 69632 B >= 2 stages (65536 B)
 template <int EPI>
@@ -478,31 +340,6 @@ static void gemm2_f32_launch(const float* A, const float* W, const float* bias, 
   const int tiles_n = (N + F2_BN - 1) / F2_BN, nblk = tiles_n * ((M + F2_BM - 1) / F2_BM);
   hipLaunchKernelGGL(k_gemm2_f32<EPI>, dim3((unsigned)nblk), dim3(256), F2_LDS, st, A, W, bias, resid, out, M, N, K,
                      tiles_n, nblk);
-}
-
-template <int EPI, int FBN>
-static void gemm3_f32_launch(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
-                             int N, int K, hipStream_t st) {
-  const int tiles_n = (N + FBN - 1) / FBN, nblk = tiles_n * ((M + BM - 1) / BM);
-  hipLaunchKernelGGL((k_gemm3_f32<EPI, FBN>), dim3((unsigned)nblk), dim3(512), f_lds<FBN>(), st, A, W, bias, resid,
-                     out, M, N, K, tiles_n, nblk);
-}
-// 128 or 64 columns per block: the one whose last wave of blocks (one block
-// per CU, 256 CUs) is fuller, 128 unless 64 wastes clearly less
-static int f32_block_cols(int M, int N) {
-  auto waste = [&](int bn) {
-    const long tiles = (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM);
-    return (double)((tiles + 255) / 256 * 256) / (double)tiles;
-  };
-  return waste(64) < waste(128) - 0.03 ? 64 : 128;
-}
-template <int EPI>
-static void gemm3_f32_auto(const float* A, const float* W, const float* bias, const float* resid, float* out, int M,
-                           int N, int K, hipStream_t st) {
-  if (f32_block_cols(M, N) == 64)
-    gemm3_f32_launch<EPI, 64>(A, W, bias, resid, out, M, N, K, st);
-  else
-    gemm3_f32_launch<EPI, 128>(A, W, bias, resid, out, M, N, K, st);
 }
 
 // ---- fused attention (flash-style) ------------------------------------------
@@ -942,12 +779,9 @@ int fhe_bert_create(const fhe_bert_config* c, int device, fhe_bert** out) {
       hipFuncSetAttribute((const void*)k_gemm3<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
       hipFuncSetAttribute((const void*)k_gemm3<EPI_GELU_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
       hipFuncSetAttribute((const void*)k_gemm3<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, G3_LDS) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<128>()) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_GELU_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<128>()) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_RESID_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<128>()) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_F32, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<64>()) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_GELU_F32, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<64>()) ||
-      hipFuncSetAttribute((const void*)k_gemm3_f32<EPI_RESID_F32, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<64>()) ||
+      hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_GELU_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS) ||
+      hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS) ||
       hipFuncSetAttribute((const void*)k_attention<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ||
       hipFuncSetAttribute((const void*)k_attention<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024))
     rc = FHE_E_DEVICE;
@@ -1146,7 +980,7 @@ static int gemm_f32(fhe_bert* h, const float* A, const float* W, const float* bi
                     int M, int N, int K, hipStream_t st) {
   hipEvent_t e1;
   pbegin(h, h->p_gemm, st, &e1);
-  gemm3_f32_auto<EPI>(A, W, bias, resid, out, M, N, K, st);
+  gemm2_f32_launch<EPI>(A, W, bias, resid, out, M, N, K, st);
   pend(h, h->p_gemm, st, e1, 2.0 * M * N * K);
   BCHK(h, hipGetLastError());
   return FHE_OK;

@@ -180,21 +180,42 @@ __device__ __forceinline__ u64 ahat_w(const u64* A, int m, int N) {
   const u64 r = m < 0 ? (u64)0 - v : v;
   return m < N ? r : 0;
 }
+// weights: lane l of the wave holds w[64 c + l] of the current 64-feature
+// block c (one coalesced load per 64 features; whole waves call this: kN / 8
+// threads is a multiple of 64) and feature j's weight is broadcast by
+// v_readlane, no memory access in the MAC loop (FHEICP_EL_WREG=0, A/B
+// builds: a load per feature at a clamped index)
+#ifndef FHEICP_EL_WREG
+#define FHEICP_EL_WREG 1
+#endif
+__device__ __forceinline__ u64 readlane64(u64 v, int lane) {
+  return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+}
 __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const int64_t* __restrict__ w, int Dg,
                                             u64 acc[8]) {
   u64 win[16];
 #pragma unroll
   for (int q = 0; q < 8; ++q) win[q] = ahat_w(A, q - u0 - 7, N);
+  [[maybe_unused]] u64 wreg = 0;
+  [[maybe_unused]] const int lane = threadIdx.x & 63;
   for (int j0 = 0; j0 < Dg; j0 += 8) {
+    if (FHEICP_EL_WREG && (j0 & 63) == 0) {
+      const int jl = j0 + lane;
+      wreg = jl < Dg ? (u64)w[jl] : 0;  // 0 past Dg: those features weigh nothing
+    }
 #pragma unroll
     for (int q = 8; q < 16; ++q) win[q] = ahat_w(A, j0 + q - u0 - 7, N);
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      // the weight of feature j0 + jj (0 past Dg), read at a clamped index
-      // (wave-uniform: one scalar load)
-      const int j = j0 + jj;
-      const u64 wl = (u64)w[j < Dg ? j : Dg - 1];
-      const u64 wj = j < Dg ? wl : 0;
+      u64 wj;
+      if constexpr (FHEICP_EL_WREG) {
+        wj = readlane64(wreg, (j0 & 63) + jj);
+      } else {
+        const int j = j0 + jj;
+        const u64 wl = (u64)w[j < Dg ? j : Dg - 1];
+        wj = j < Dg ? wl : 0;
+      }
 #pragma unroll
       for (int r = 0; r < 8; ++r) acc[r] += wj * win[jj + 7 - r];
     }
@@ -298,7 +319,10 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 // bit-identical to the two kernels. The features' noise blocks go to a fifth
 // wave: on a mask thread, the two of D = 16 made its wave three blocks long
 // against one for the rest (27 us per 1024 pairs, 0.18 of the VALU roof).
-constexpr int EL_THREADS = 320;
+#ifndef FHEICP_EL_NOISE_WAVE
+#define FHEICP_EL_NOISE_WAVE 1  // 0 (A/B builds): the noise blocks on threads 0.. of the mask waves
+#endif
+constexpr int EL_THREADS = FHEICP_EL_NOISE_WAVE ? 320 : 256;
 __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big, const int64_t* __restrict__ x,
                                                         int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
@@ -319,7 +343,8 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
       for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
     }
     // the features' noise words, 8 per block, on wave 4
-    for (int blk = (int)threadIdx.x - 256; blk >= 0 && 8 * blk < Dg; blk += EL_THREADS - 256) {
+    for (int blk = FHEICP_EL_NOISE_WAVE ? (int)threadIdx.x - 256 : (int)threadIdx.x; blk >= 0 && 8 * blk < Dg;
+         blk += FHEICP_EL_NOISE_WAVE ? EL_THREADS - 256 : 256) {
       u64 e[8];
       stream_block(K, TAG_ENC_NOISE, id, (uint32_t)blk, e);
 #pragma unroll

@@ -1,5 +1,5 @@
 // Probe of the BERT GEMMs (fhe-icp_amd/csrc/bert.hip k_gemm3, bf16, and
-// k_gemm3_f32, f32) at the embed bench's shapes (25.6k tokens, random
+// k_gemm2_f32, f32) at the embed bench's shapes (25.6k tokens, random
 // operands): HIP-event time per launch and TFLOP/s.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DFBERT_AB_NOEPI] tools/gemm_probe.hip -o gemm_probe
 #include "../fhe-icp_amd/csrc/bert.hip"
@@ -70,36 +70,6 @@ int main() {
   }
   const int fshapes[4][3] = {{2304, 768, EPI_F32}, {768, 768, EPI_RESID_F32}, {3072, 768, EPI_GELU_F32},
                              {768, 3072, EPI_RESID_F32}};
-#define FATTR(E, B) hipFuncSetAttribute((const void*)k_gemm3_f32<E, B>, hipFuncAttributeMaxDynamicSharedMemorySize, f_lds<B>())
-  FATTR(EPI_F32, 128); FATTR(EPI_GELU_F32, 128); FATTR(EPI_RESID_F32, 128);
-  FATTR(EPI_F32, 64); FATTR(EPI_GELU_F32, 64); FATTR(EPI_RESID_F32, 64);
-  for (int bn : {128, 64}) {
-    for (auto& sh : fshapes) {
-      const int N = sh[0], K = sh[1], epi = sh[2];
-      float* o = (float*)out;
-      auto run = [&]() {
-        if (bn == 128) {
-          if (epi == EPI_F32) gemm3_f32_launch<EPI_F32, 128>(Af, Wf, bias, resid, o, M, N, K, 0);
-          else if (epi == EPI_GELU_F32) gemm3_f32_launch<EPI_GELU_F32, 128>(Af, Wf, bias, resid, o, M, N, K, 0);
-          else gemm3_f32_launch<EPI_RESID_F32, 128>(Af, Wf, bias, resid, o, M, N, K, 0);
-        } else {
-          if (epi == EPI_F32) gemm3_f32_launch<EPI_F32, 64>(Af, Wf, bias, resid, o, M, N, K, 0);
-          else if (epi == EPI_GELU_F32) gemm3_f32_launch<EPI_GELU_F32, 64>(Af, Wf, bias, resid, o, M, N, K, 0);
-          else gemm3_f32_launch<EPI_RESID_F32, 64>(Af, Wf, bias, resid, o, M, N, K, 0);
-        }
-      };
-      run();
-      hipEventRecord(e0, 0);
-      for (int r = 0; r < 10; ++r) run();
-      hipEventRecord(e1, 0);
-      hipEventSynchronize(e1);
-      float ms = 0;
-      hipEventElapsedTime(&ms, e0, e1);
-      ms /= 10;
-      printf("f32 BN=%d N=%d K=%d epi=%d: %.1f us, %.1f TF/s (auto picks BN=%d)\n", bn, N, K, epi, ms * 1e3,
-             2.0 * M * N * K / (ms * 1e-3) / 1e12, f32_block_cols(M, N));
-    }
-  }
   hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
   hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_GELU_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
   hipFuncSetAttribute((const void*)k_gemm2_f32<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
@@ -119,7 +89,7 @@ int main() {
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     ms /= 10;
-    printf("f32 k_gemm2 128x128x2wg N=%d K=%d epi=%d: %.1f us, %.1f TF/s\n", N, K, epi, ms * 1e3,
+    printf("f32 k_gemm2_f32 N=%d K=%d epi=%d: %.1f us, %.1f TF/s\n", N, K, epi, ms * 1e3,
            2.0 * M * N * K / (ms * 1e-3) / 1e12);
   }
   return 0;

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """gfx950 ISA checks of the LDS-DMA pipelines (no GPU): in every
-k_gemm3 / k_gemm3_f32 instantiation, no `s_waitcnt vmcnt(0)` may sit between
+k_gemm3 / k_gemm2_f32 instantiation, no `s_waitcnt vmcnt(0)` may sit between
 the global_load_lds of the next K step and the first ds_read of the current
 one (hipcc drains the DMA pipeline there when the reads' type may alias the
 DMA's, e.g. HIP's float4 struct; cdna_hip_programming.md §5 trap 4).

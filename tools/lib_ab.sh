@@ -13,7 +13,8 @@ for rep in ${REPS:-1 2}; do
 import json; d=json.load(open('$o'))
 p=d.get('parity',{})
 print('${TAG:-c2} $name rep$rep', d['value'], d['ms_per_step'], 'parity', all(v for k,v in p.items() if isinstance(v,bool)),
-      ' '.join(f\"{k}:{v.get('kernel')}={v.get('avg_launch_ms')}\" for k,v in d['roofline'].get('kernels',{}).items()))
+      ' '.join(f\"{k}:{v.get('kernel')}={v.get('avg_launch_ms')}\" for k,v in d['roofline'].get('kernels',{}).items()),
+      'leveled', d['leveled_score']['value'], d['leveled_score']['roofline']['avg_launch_ms'], d['leveled_score']['acc_equal_to_compare'])
 "
   done
 done
