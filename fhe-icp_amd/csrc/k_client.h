@@ -180,27 +180,38 @@ __device__ __forceinline__ u64 ahat_w(const u64* A, int m, int N) {
   const u64 r = m < 0 ? (u64)0 - v : v;
   return m < N ? r : 0;
 }
-// weights: lane l of the wave holds w[64 c + l] of the current 64-feature
-// block c (one coalesced load per 64 features; whole waves call this: kN / 8
-// threads is a multiple of 64) and feature j's weight is broadcast by
-// v_readlane, no memory access in the MAC loop (FHEICP_EL_WREG=0, A/B
-// builds: a load per feature at a clamped index)
-#ifndef FHEICP_EL_WREG
-#define FHEICP_EL_WREG 1
-#endif
 __device__ __forceinline__ u64 readlane64(u64 v, int lane) {
   return ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
 }
+// Weights: lane l of the wave holds w[64 c + l] of the current 64-feature
+// block c (one coalesced load per 64 features; whole waves call this: kN / 8
+// threads is a multiple of 64) and feature j's weight is broadcast by
+// v_readlane into scalar registers, so the MAC loop touches no memory but the
+// window's LDS reads (a clamped global load per feature instead: 38 us per
+// 1024 pairs against 26, docs/AB_LOG_r04.md).
+// The product w a mod 2^64 is split by the halves of a: with w = wlo + 2^32 whi,
+//   w a = wlo alo + 2^32 (wlo ahi + whi alo)   (mod 2^64),
+// the first term a 64-bit v_mad_u64_u32 into lo[r], the second only mod 2^32
+// into hi[r]; whi is wave-uniform, 0 or all-ones for |w| < 2^31 (every
+// quantized weight), so its term is a scalar branch: nothing, or hi -= alo.
+// One 32-bit multiply per product instead of the three of a full u64 one.
+#ifndef FHEICP_EL_HI_MASK
+#define FHEICP_EL_HI_MASK 0  // 1 (A/B builds): hi -= alo & whi, branch only for |w| >= 2^31
+#endif
 __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const int64_t* __restrict__ w, int Dg,
                                             u64 acc[8]) {
   u64 win[16];
+  u64 lo[8];
+  uint32_t hi[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) lo[r] = acc[r], hi[r] = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) win[q] = ahat_w(A, q - u0 - 7, N);
-  [[maybe_unused]] u64 wreg = 0;
-  [[maybe_unused]] const int lane = threadIdx.x & 63;
+  u64 wreg = 0;
+  const int lane = threadIdx.x & 63;
   for (int j0 = 0; j0 < Dg; j0 += 8) {
-    if (FHEICP_EL_WREG && (j0 & 63) == 0) {
+    if ((j0 & 63) == 0) {
       const int jl = j0 + lane;
       wreg = jl < Dg ? (u64)w[jl] : 0;  // 0 past Dg: those features weigh nothing
     }
@@ -208,20 +219,37 @@ __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const i
     for (int q = 8; q < 16; ++q) win[q] = ahat_w(A, j0 + q - u0 - 7, N);
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      u64 wj;
-      if constexpr (FHEICP_EL_WREG) {
-        wj = readlane64(wreg, (j0 & 63) + jj);
-      } else {
-        const int j = j0 + jj;
-        const u64 wl = (u64)w[j < Dg ? j : Dg - 1];
-        wj = j < Dg ? wl : 0;
-      }
+      const u64 wj = readlane64(wreg, (j0 & 63) + jj);
+      const uint32_t wlo = (uint32_t)wj, whi = (uint32_t)(wj >> 32);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) acc[r] += wj * win[jj + 7 - r];
+      for (int r = 0; r < 8; ++r) {
+        const u64 a = win[jj + 7 - r];
+        lo[r] += (u64)wlo * (uint32_t)a;
+        hi[r] += wlo * (uint32_t)(a >> 32);
+      }
+#if FHEICP_EL_HI_MASK
+      if (whi + 1u > 1u) {  // |w| >= 2^31: the general term
+#pragma unroll
+        for (int r = 0; r < 8; ++r) hi[r] += whi * (uint32_t)win[jj + 7 - r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) hi[r] -= (uint32_t)win[jj + 7 - r] & whi;
+      }
+#else
+      if (whi == 0xffffffffu) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) hi[r] -= (uint32_t)win[jj + 7 - r];
+      } else if (whi != 0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) hi[r] += whi * (uint32_t)win[jj + 7 - r];
+      }
+#endif
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) win[q] = win[q + 8];
   }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc[r] = lo[r] + ((u64)hi[r] << 32);
 }
 
 // Client side: GLWE encryption of the packed features (fhe_encrypt_packed_batch).
@@ -316,13 +344,12 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 // computed from it: Extract_0(B W_g) = <a_g, s> + sum_t w_t (m_t + e_t)
 // exactly (mod 2^64), so
 //   b = <a, s> + sum_j w_j (x_j Delta + e_j) + cst Delta,
-// bit-identical to the two kernels. The features' noise blocks go to a fifth
-// wave: on a mask thread, the two of D = 16 made its wave three blocks long
-// against one for the rest (27 us per 1024 pairs, 0.18 of the VALU roof).
-#ifndef FHEICP_EL_NOISE_WAVE
-#define FHEICP_EL_NOISE_WAVE 1  // 0 (A/B builds): the noise blocks on threads 0.. of the mask waves
-#endif
-constexpr int EL_THREADS = FHEICP_EL_NOISE_WAVE ? 320 : 256;
+// bit-identical to the two kernels. The features' noise blocks (ceil(Dg / 8)
+// of them) follow the mask blocks on one thread per wave, starting at wave
+// b mod 4: a wave that carries one runs two ChaCha20 blocks, and the rotation
+// spreads those waves over the SIMDs across the workgroups of a CU (a fifth
+// wave for them measured 28 us per 1024 pairs against 26, docs/AB_LOG_r04.md).
+constexpr int EL_THREADS = 256;
 __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big, const int64_t* __restrict__ x,
                                                         int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
@@ -336,15 +363,16 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
     const u64 id = id0 + (u64)b * G + g;
     const int Dg = min(D - g * N, N);
     __syncthreads();  // the previous chunk's readers are done
-    for (int blk = threadIdx.x; blk < k * N / 8 && threadIdx.x < 256; blk += 256) {
+    for (int blk = threadIdx.x; blk < k * N / 8; blk += 256) {
       u64 m[8];
       stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
 #pragma unroll
       for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
     }
-    // the features' noise words, 8 per block, on wave 4
-    for (int blk = FHEICP_EL_NOISE_WAVE ? (int)threadIdx.x - 256 : (int)threadIdx.x; blk >= 0 && 8 * blk < Dg;
-         blk += FHEICP_EL_NOISE_WAVE ? EL_THREADS - 256 : 256) {
+    // the features' noise words, 8 per block: block nb on lane nb / 4 of wave
+    // (nb + b) mod 4
+    const int wv = (int)(threadIdx.x >> 6), ln = (int)(threadIdx.x & 63);
+    for (int blk = 4 * ln + ((wv - (int)(b & 3)) & 3); 8 * blk < Dg; blk += 256) {
       u64 e[8];
       stream_block(K, TAG_ENC_NOISE, id, (uint32_t)blk, e);
 #pragma unroll

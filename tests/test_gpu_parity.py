@@ -496,13 +496,16 @@ def test_encrypt_linear_fused_bit_exact(which, request):
     fhe_linear_packed_batch, and both to the oracle's textbook GLWE encryption
     + product + sample extraction; GLWEs equal the oracle's word for word. D
     covers a count that is not a multiple of anything (37), the compare
-    path's 16, and more features than N (two GLWEs per row)."""
+    path's 16, and more features than N (two GLWEs per row); the last case
+    draws weights over the whole int64 range (the MAC's general high-word
+    term, |w| >= 2^31) and is checked word for word only (its message wraps)."""
     eng, ref = request.getfixturevalue(which)
     rng = np.random.default_rng(11)
     N = eng.params.N
-    for B, D in ((5, 37), (64, 16), (3, N + 44)):
+    for B, D in ((5, 37), (64, 16), (3, N + 44), (4, 70)):
         x = rng.integers(-32, 32, (B, D))
-        w = rng.integers(-127, 128, D)
+        wide = D == 70
+        w = rng.integers(-2 ** 63, 2 ** 63 - 1, D) if wide else rng.integers(-127, 128, D)
         cst = int(rng.integers(-1000, 1000))
         fused = u64(eng.encrypt_linear(x, w, cst, seed=8, id0=77))
         glwe = eng.encrypt_packed(x, seed=8, id0=77)
@@ -512,5 +515,7 @@ def test_encrypt_linear_fused_bit_exact(which, request):
         assert np.array_equal(fused, two), (B, D)
         lin_ref = ref.linear_packed(glwe_ref, D, w, cst)
         assert np.array_equal(fused, lin_ref), (B, D)
+        if wide:
+            continue
         half = 2 ** (eng.msg_bits - 1)
         assert np.array_equal(ref.decrypt_ints(lin_ref), (x @ w + cst + half) % (2 * half) - half)
