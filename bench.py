@@ -878,7 +878,7 @@ def embed_main(args, world, rank, local, dev):
         "config": {"workload": f"bert-base forward, {B} sequences x {S} tokens per GPU, mean pooling",
                    "batch": B, "seq_len": S, "tokens_per_step": B * S * world, "parallelism": f"replicas{world}"},
         "tokens_per_sec": round(seqs * S / elapsed, 1),
-        "roofline": {"bound": "mfma", "kernel": "fbert::k_gemm3_f32<EPI>" if prec == "f32" else "fbert::k_gemm3<EPI>",
+        "roofline": {"bound": "mfma", "kernel": "fbert::k_gemm2_f32<EPI>" if prec == "f32" else "fbert::k_gemm3<EPI>",
                      "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                      "traffic": None, "gemm_ms_per_step": round(gm["total_ms"] / args.steps, 3),
                      "gemm_launches_per_step": gm["launches"] // max(args.steps, 1),

@@ -1,5 +1,5 @@
 """Library GEMM rate (torch.matmul -> hipBLASLt) on the BERT encoder shapes, as the
-yardstick for k_gemm3 / k_gemm3_f32 (tokens M = 256 x 100; QKV, attention output,
+yardstick for k_gemm3 / k_gemm2_f32 (tokens M = 256 x 100; QKV, attention output,
 FFN1, FFN2). Usage: python tools/blas_probe.py [bf16|f32] (f32: exact fp32, the
 reference's arithmetic; no TF32 path exists on gfx950 and it is disabled here)."""
 import sys
