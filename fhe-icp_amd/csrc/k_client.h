@@ -189,23 +189,13 @@ __device__ __forceinline__ u64 readlane64(u64 v, int lane) {
 // threads is a multiple of 64) and feature j's weight is broadcast by
 // v_readlane into scalar registers, so the MAC loop touches no memory but the
 // window's LDS reads (a clamped global load per feature instead: 38 us per
-// 1024 pairs against 26, docs/AB_LOG_r04.md).
-// The product w a mod 2^64 is split by the halves of a: with w = wlo + 2^32 whi,
-//   w a = wlo alo + 2^32 (wlo ahi + whi alo)   (mod 2^64),
-// the first term a 64-bit v_mad_u64_u32 into lo[r], the second only mod 2^32
-// into hi[r]; whi is wave-uniform, 0 or all-ones for |w| < 2^31 (every
-// quantized weight), so its term is a scalar branch: nothing, or hi -= alo.
-// One 32-bit multiply per product instead of the three of a full u64 one.
-#ifndef FHEICP_EL_HI_MASK
-#define FHEICP_EL_HI_MASK 0  // 1 (A/B builds): hi -= alo & whi, branch only for |w| >= 2^31
-#endif
+// 1024 pairs against 26, docs/AB_LOG_r04.md). The u64 product is the
+// compiler's v_mad_u64_u32 + two v_mul_lo_u32 + v_add3_u32: splitting it by
+// the halves of the mask word into two v_mad_u64_u32 measured slower (the MAC
+// phase 5,740 cycles against 5,010, docs/AB_LOG_r04.md).
 __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const int64_t* __restrict__ w, int Dg,
                                             u64 acc[8]) {
   u64 win[16];
-  u64 lo[8];
-  uint32_t hi[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) lo[r] = acc[r], hi[r] = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) win[q] = ahat_w(A, q - u0 - 7, N);
   u64 wreg = 0;
@@ -220,36 +210,12 @@ __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const i
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const u64 wj = readlane64(wreg, (j0 & 63) + jj);
-      const uint32_t wlo = (uint32_t)wj, whi = (uint32_t)(wj >> 32);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const u64 a = win[jj + 7 - r];
-        lo[r] += (u64)wlo * (uint32_t)a;
-        hi[r] += wlo * (uint32_t)(a >> 32);
-      }
-#if FHEICP_EL_HI_MASK
-      if (whi + 1u > 1u) {  // |w| >= 2^31: the general term
-#pragma unroll
-        for (int r = 0; r < 8; ++r) hi[r] += whi * (uint32_t)win[jj + 7 - r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) hi[r] -= (uint32_t)win[jj + 7 - r] & whi;
-      }
-#else
-      if (whi == 0xffffffffu) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) hi[r] -= (uint32_t)win[jj + 7 - r];
-      } else if (whi != 0) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) hi[r] += whi * (uint32_t)win[jj + 7 - r];
-      }
-#endif
+      for (int r = 0; r < 8; ++r) acc[r] += wj * win[jj + 7 - r];
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) win[q] = win[q + 8];
   }
-#pragma unroll
-  for (int r = 0; r < 8; ++r) acc[r] = lo[r] + ((u64)hi[r] << 32);
 }
 
 // Client side: GLWE encryption of the packed features (fhe_encrypt_packed_batch).
@@ -345,11 +311,33 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 // exactly (mod 2^64), so
 //   b = <a, s> + sum_j w_j (x_j Delta + e_j) + cst Delta,
 // bit-identical to the two kernels. The features' noise blocks (ceil(Dg / 8)
-// of them) follow the mask blocks on one thread per wave, starting at wave
-// b mod 4: a wave that carries one runs two ChaCha20 blocks, and the rotation
-// spreads those waves over the SIMDs across the workgroups of a CU (a fifth
-// wave for them measured 28 us per 1024 pairs against 26, docs/AB_LOG_r04.md).
+// of them) follow the mask blocks on threads 0.. (a fifth wave for them
+// measured 28 us per 1024 pairs against 26; rotating them over the waves by
+// pair, 28.7, docs/AB_LOG_r04.md). The key words of the thread's eight mask
+// words are loaded at the start, behind the ChaCha20 work.
+// Launched with EL_LDS bytes of LDS, which admits at most four workgroups per
+// CU: the phase stamps (tools/el_stamps.py) showed workgroups of one launch
+// running 10 to 24 us as CUs took 2 to 5 of them; four per CU of 1024 pairs
+// deal them out evenly.
 constexpr int EL_THREADS = 256;
+constexpr int EL_LDS = 36 * 1024;
+// A/B builds (FHEICP_AB): per wave of the first 1024 workgroups, {s_memrealtime
+// at start, s_memtime at start / after the mask blocks / after the noise blocks
+// / after the barrier / after the MAC loop / at the end, s_memrealtime at the
+// end} (tools/el_stamps.py, fhe_debug_el_stamps)
+#ifdef FHEICP_AB
+__device__ unsigned long long g_el_stamps[1024][4][8];
+#define EL_STAMP(k, t)                  \
+  do {                                  \
+    __builtin_amdgcn_sched_barrier(0);  \
+    st_[k] = (t);                       \
+    __builtin_amdgcn_sched_barrier(0);  \
+  } while (0)
+#else
+#define EL_STAMP(k, t) \
+  do {                 \
+  } while (0)
+#endif
 __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big, const int64_t* __restrict__ x,
                                                         int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
@@ -357,6 +345,13 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
   extern __shared__ u64 shm[];
   __shared__ u64 red[EL_THREADS / 64];
   const int64_t b = blockIdx.x;
+  [[maybe_unused]] unsigned long long st_[8];
+  EL_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  EL_STAMP(1, __builtin_amdgcn_s_memtime());
+  const int t8 = 8 * threadIdx.x;
+  u64 key[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) key[q] = t8 < k * N ? s_big[t8 + q] : 0;
   u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 bpart = 0;
   for (int g = 0; g < G; ++g) {
@@ -369,10 +364,9 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
 #pragma unroll
       for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
     }
-    // the features' noise words, 8 per block: block nb on lane nb / 4 of wave
-    // (nb + b) mod 4
-    const int wv = (int)(threadIdx.x >> 6), ln = (int)(threadIdx.x & 63);
-    for (int blk = 4 * ln + ((wv - (int)(b & 3)) & 3); 8 * blk < Dg; blk += 256) {
+    EL_STAMP(2, __builtin_amdgcn_s_memtime());
+    // the features' noise words, 8 per block
+    for (int blk = threadIdx.x; 8 * blk < Dg; blk += 256) {
       u64 e[8];
       stream_block(K, TAG_ENC_NOISE, id, (uint32_t)blk, e);
 #pragma unroll
@@ -383,21 +377,33 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
                    (((u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits)) + (u64)tuniform(e[q], noise_bits));
       }
     }
+    EL_STAMP(3, __builtin_amdgcn_s_memtime());
     __syncthreads();
+    EL_STAMP(4, __builtin_amdgcn_s_memtime());
     packed_chunk_mask(shm, N, k, w + g * N, Dg, acc);
+    EL_STAMP(5, __builtin_amdgcn_s_memtime());
   }
-  const int t8 = 8 * threadIdx.x;
   u64* o = out + (size_t)b * (k * N + 1);
   u64 sdot = 0;
   if (t8 < k * N) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       o[t8 + q] = acc[q];
-      sdot += acc[q] & (0 - s_big[t8 + q]);
+      sdot += acc[q] & (0 - key[q]);
     }
   }
   const u64 tot = block_sum_u64<EL_THREADS>(sdot + bpart, red);
   if (threadIdx.x == 0) o[k * N] = tot + cst_scaled;
+#ifdef FHEICP_AB
+  EL_STAMP(6, __builtin_amdgcn_s_memtime());
+  EL_STAMP(7, __builtin_amdgcn_s_memrealtime());
+  if ((threadIdx.x & 63) < 8 && b < 1024) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v = (int)(threadIdx.x & 63) == q ? st_[q] : v;
+    g_el_stamps[b][threadIdx.x >> 6][threadIdx.x & 63] = v;
+  }
+#endif
 }
 
 // A seeded LWE keeps only its body; the mask is stream(TAG_ENC_MASK, id) of

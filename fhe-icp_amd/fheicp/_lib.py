@@ -92,6 +92,7 @@ SIGNATURES = [
     ("fhe_memcpy_d2h", C.c_int, [_CTXP, _vp, _vp, C.c_size_t, _vp]),
     ("fhe_stream_sync", C.c_int, [_CTXP, _vp]),
     ("fhe_debug_v4_stamps", C.c_int, [_CTXP, _vp]),
+    ("fhe_debug_el_stamps", C.c_int, [_CTXP, _vp]),
     ("fhe_profile_enable", C.c_int, [_CTXP, C.c_int]),
     ("fhe_profile_read", C.c_int, [_CTXP, C.c_char_p, C.POINTER(C.c_double), C.POINTER(_i64), C.POINTER(_i64)]),
     ("fhe_profile_kernel_name", C.c_int, [_CTXP, C.c_char_p, C.c_char_p, C.c_size_t]),

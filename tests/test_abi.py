@@ -124,6 +124,7 @@ def test_build_info_and_kernel_names_on_host_context():
     assert L.fhe_pbs_table_batch(h, None, 0, None, 4, None, None) == -2
     assert L.fhe_threshold_batch(h, None, 0, 0, None, None) == -2
     assert L.fhe_debug_v4_stamps(h, buf) == -2
+    assert L.fhe_debug_el_stamps(h, buf) == -2
     L.fhe_ctx_destroy(h)
 
 
