@@ -495,14 +495,35 @@ CHACHA_BLOCK_OPS = 976  # one ChaCha20 block: 80 quarter rounds x 12 (add, xor, 
 U64_MAC_OPS = 4         # acc += w * a mod 2^64, small signed w: v_mad_u64_u32 + 2 v_mul_lo_u32 + v_add3_u32
 
 
+# Issue rates of k_encrypt_linear's instructions at its occupancy (4 waves per
+# SIMD), T lane-ops/s chip-wide, measured by tools/valu_probe.hip
+# (profiles/r04_valu_probe.txt): VOP2 add/xor dual-issue, the VOP3 ops
+# (v_alignbit_b32, v_mul_lo_u32, v_add3_u32, v_mad_u64_u32) do not.
+VALU_RATES_4W = {"add": 57.36, "xor": 58.57, "alignbit": 36.47, "mad_u64": 31.63, "mul_lo": 34.87, "add3": 35.46}
+
+
+def leveled_blocks_per_pair(p, D: int) -> int:
+    G = -(-D // p.N)
+    return G * (p.k * p.N // 8) + sum(-(-min(D - g * p.N, p.N) // 8) for g in range(G))
+
+
+def leveled_mix_floor_s(p, D: int, B: int) -> float:
+    """Seconds a launch of B pairs needs at the measured issue rate of every
+    instruction of its ops model: a ChaCha20 block is 336 v_add_u32, 320
+    v_xor_b32 and 320 v_alignbit_b32; a u64 MAC one v_mad_u64_u32, two
+    v_mul_lo_u32 and one v_add3_u32."""
+    r = {k: v * 1e12 for k, v in VALU_RATES_4W.items()}
+    chacha = 336 / r["add"] + 320 / r["xor"] + 320 / r["alignbit"]
+    mac = 1 / r["mad_u64"] + 2 / r["mul_lo"] + 1 / r["add3"]
+    return B * (leveled_blocks_per_pair(p, D) * chacha + p.k * p.N * D * mac)
+
+
 def leveled_ops_per_pair(p, D: int) -> int:
     """Algorithmic 32-bit integer ops of one pair in k_encrypt_linear (packed
     features): the GLWE masks (kN / 8 ChaCha20 blocks per
     chunk), the features' noise words (ceil(Dg / 8) blocks per chunk) and the
     extraction's D x kN u64 multiply-adds."""
-    G = -(-D // p.N)
-    blocks = G * (p.k * p.N // 8) + sum(-(-min(D - g * p.N, p.N) // 8) for g in range(G))
-    return CHACHA_BLOCK_OPS * blocks + U64_MAC_OPS * p.k * p.N * D
+    return CHACHA_BLOCK_OPS * leveled_blocks_per_pair(p, D) + U64_MAC_OPS * p.k * p.N * D
 
 
 def leveled_score(args, model, q_dev, d_dev, acc_compare) -> dict:
@@ -545,6 +566,9 @@ def leveled_score(args, model, q_dev, d_dev, acc_compare) -> dict:
                          "launches": k["launches"], "pairs_per_launch": B,
                          "ops_per_pair": leveled_ops_per_pair(p, args.dim),
                          "ops_model": f"{CHACHA_BLOCK_OPS} per ChaCha20 block + {U64_MAC_OPS} per u64 MAC",
+                         "valu_mix_floor_ms": round(leveled_mix_floor_s(p, args.dim, B) * 1e3, 5),
+                         "mix_frac": round(leveled_mix_floor_s(p, args.dim, B) / avg_s, 4) if k["launches"] else 0.0,
+                         "mix_rates": "tools/valu_probe.hip at 4 waves/SIMD (profiles/r04_valu_probe.txt)",
                          "pmc_valu_lane_ops_per_launch": pmc_ops,
                          "pmc_executed_frac": round(pmc_ops / avg_s / 1e12 / VALU_PEAK_TOPS, 4)
                          if pmc_ops and k["launches"] else None,

@@ -808,8 +808,7 @@ int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_enc, (hipStream_t)stream, &e1);
   ctx->prof_enc.kernel = "k_encrypt_linear";
-  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(EL_THREADS), std::max((size_t)p.k * p.N * 8, (size_t)EL_LDS),
-                     (hipStream_t)stream, K, p.N,
+  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(EL_THREADS), (size_t)p.k * p.N * 8, (hipStream_t)stream, K, p.N,
                      p.k, p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, d_w,
                      ((u64)cst) << (64 - p.msg_bits), id0, d_out);
   prof_end(ctx, ctx->prof_enc, (hipStream_t)stream, e1, B);
@@ -1750,7 +1749,7 @@ int fhe_debug_el_stamps(fhe_ctx* ctx, uint64_t* h_out) {
   return fail(ctx, FHE_E_STATE, "phase stamps need an A/B build (FHEICP_AB, tools/build_variant.sh)");
 #else
   HIPCHK(ctx, hipDeviceSynchronize());
-  HIPCHK(ctx, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_el_stamps), sizeof(unsigned long long) * 1024 * 4 * 8));
+  HIPCHK(ctx, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_el_stamps), sizeof(unsigned long long) * 1024 * 4 * 10));
   return FHE_OK;
 #endif
 }

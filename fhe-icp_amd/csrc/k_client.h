@@ -315,12 +315,13 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 // measured 28 us per 1024 pairs against 26; rotating them over the waves by
 // pair, 28.7, docs/AB_LOG_r04.md). The key words of the thread's eight mask
 // words are loaded at the start, behind the ChaCha20 work.
-// Launched with EL_LDS bytes of LDS, which admits at most four workgroups per
-// CU: the phase stamps (tools/el_stamps.py) showed workgroups of one launch
-// running 10 to 24 us as CUs took 2 to 5 of them; four per CU of 1024 pairs
-// deal them out evenly.
+// Phase stamps (tools/el_stamps.py): a launch of 1024 pairs puts exactly four
+// workgroups on every CU and one wave of each on every SIMD; the four run
+// 19k to 47k cycles as the SIMDs issue by wave age, so a CU's span is set by
+// its total VALU work. That work is priced by tools/valu_probe.hip: the
+// half-rate v_alignbit_b32 (a third of ChaCha20) and the u64 MAC's VOP3
+// multiplies (bench.py leveled_score.roofline.valu_mix_floor_ms).
 constexpr int EL_THREADS = 256;
-constexpr int EL_LDS = 36 * 1024;
 // A/B builds (FHEICP_AB): per wave of the first 1024 workgroups, {s_memrealtime
 // at start, s_memtime at start / after the mask blocks / after the noise blocks
 // / after the barrier / after the MAC loop / at the end, s_memrealtime at the

@@ -19,8 +19,8 @@ int fhe_debug_v4_stamps(fhe_ctx* ctx, uint64_t* h_out);
 
 /* A/B builds only: k_encrypt_linear phase stamps, 1024 workgroups x 4 waves x
  * {s_memrealtime start, s_memtime at start / mask blocks done / noise blocks
- * done / after the barrier / MAC done / end, s_memrealtime end}
- * (tools/el_stamps.py); h_out holds 32768 words. FHE_E_STATE in the shipped
+ * done / after the barrier / MAC done / end, s_memrealtime end, HW_ID, XCC_ID}
+ * (tools/el_stamps.py); h_out holds 40960 words. FHE_E_STATE in the shipped
  * build. */
 int fhe_debug_el_stamps(fhe_ctx* ctx, uint64_t* h_out);
 

@@ -85,3 +85,17 @@ def test_leveled_ops_model():
     # two chunks past N features (1100 = 1024 + 76): two masks, 128 + 10 noise blocks
     assert bench.leveled_ops_per_pair(p, 1100) == (bench.CHACHA_BLOCK_OPS * (2 * kN // 8 + 128 + 10)
                                                    + bench.U64_MAC_OPS * kN * 1100)
+
+
+def test_leveled_mix_floor():
+    """The mix-aware floor of k_encrypt_linear: blocks x (ChaCha20 at the
+    measured add / xor / alignbit rates) + MACs x (mad_u64 + 2 mul_lo + add3),
+    linear in the pairs; the plain ops model at the dual-issue peak is faster."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    from fheicp.params import params_for_bits
+    p = params_for_bits(16)
+    assert bench.leveled_blocks_per_pair(p, 16) == 258
+    f1 = bench.leveled_mix_floor_s(p, 16, 1)
+    assert abs(bench.leveled_mix_floor_s(p, 16, 1024) - 1024 * f1) < 1e-15
+    assert f1 > bench.leveled_ops_per_pair(p, 16) / (bench.VALU_PEAK_TOPS * 1e12)

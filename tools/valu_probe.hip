@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
+#include "../fhe-icp_amd/csrc/prng.h"
+
 #define CHK(x)                                                                   \
   do {                                                                           \
     hipError_t e = (x);                                                          \
@@ -43,6 +45,22 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, unsigned seed) {
     if constexpr (OP == 5) { OP8(MAD) }
     if constexpr (OP == 6) { OP8(AD3) }
     if constexpr (OP == 7) { OP8(ADD) OP8(XOR) OP8(ALB) }  // ChaCha20's mix, 1:1:1
+    if constexpr (OP >= 8) {  // the product's ChaCha20 block (976 ops), 1 or 2 per step
+      if ((i & 7) == 0) {
+        fhei::ChaKey K;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) K.w[q] = seed + q;
+        uint32_t o[16], o2[16];
+        fhei::chacha20_block(K, x[0], 7u, ((unsigned long long)i << 32) | threadIdx.x, o);
+        if constexpr (OP == 9) fhei::chacha20_block(K, x[1], 8u, ((unsigned long long)i << 32) | threadIdx.x, o2);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] ^= o[q] ^ o[q + 8];
+        if constexpr (OP == 9) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] += o2[q] ^ o2[q + 8];
+        }
+      }
+    }
   }
   unsigned r = 0;
 #pragma unroll
@@ -83,7 +101,8 @@ int main() {
     if (run<0>("v_add_u32", 8, blocks, d) || run<1>("v_xor_b32", 8, blocks, d) ||
         run<2>("v_alignbit_b32", 8, blocks, d) || run<3>("v_add_f32", 8, blocks, d) ||
         run<4>("v_mul_lo_u32", 8, blocks, d) || run<5>("v_mad_u64_u32", 8, blocks, d) ||
-        run<6>("v_add3_u32", 8, blocks, d) || run<7>("add/xor/alignbit 1:1:1", 24, blocks, d))
+        run<6>("v_add3_u32", 8, blocks, d) || run<7>("add/xor/alignbit 1:1:1", 24, blocks, d) ||
+        run<8>("chacha20 x1 (976/8 per it)", 122, blocks, d) || run<9>("chacha20 x2 (976/4 per it)", 244, blocks, d))
       return 1;
   }
   return 0;
