@@ -495,11 +495,13 @@ CHACHA_BLOCK_OPS = 976  # one ChaCha20 block: 80 quarter rounds x 12 (add, xor, 
 U64_MAC_OPS = 4         # acc += w * a mod 2^64, small signed w: v_mad_u64_u32 + 2 v_mul_lo_u32 + v_add3_u32
 
 
-# Issue rates of k_encrypt_linear's instructions at its occupancy (4 waves per
-# SIMD), T lane-ops/s chip-wide, measured by tools/valu_probe.hip
+# Issue rates of k_encrypt_linear's work at its occupancy (4 waves per SIMD),
+# T lane-ops/s chip-wide, measured by tools/valu_probe.hip
 # (profiles/r04_valu_probe.txt): VOP2 add/xor dual-issue, the VOP3 ops
-# (v_alignbit_b32, v_mul_lo_u32, v_add3_u32, v_mad_u64_u32) do not.
-VALU_RATES_4W = {"add": 57.36, "xor": 58.57, "alignbit": 36.47, "mad_u64": 31.63, "mul_lo": 34.87, "add3": 35.46}
+# (v_alignbit_b32, v_mul_lo_u32, v_add3_u32, v_mad_u64_u32) do not; the
+# product's own ChaCha20 block, one per lane, runs at 37.9 (976 ops each).
+VALU_RATES_4W = {"add": 57.36, "xor": 58.57, "alignbit": 36.47, "mad_u64": 31.63, "mul_lo": 34.87, "add3": 35.46,
+                 "chacha_block": 37.91}
 
 
 def leveled_blocks_per_pair(p, D: int) -> int:
@@ -508,12 +510,12 @@ def leveled_blocks_per_pair(p, D: int) -> int:
 
 
 def leveled_mix_floor_s(p, D: int, B: int) -> float:
-    """Seconds a launch of B pairs needs at the measured issue rate of every
-    instruction of its ops model: a ChaCha20 block is 336 v_add_u32, 320
-    v_xor_b32 and 320 v_alignbit_b32; a u64 MAC one v_mad_u64_u32, two
-    v_mul_lo_u32 and one v_add3_u32."""
+    """Seconds a launch of B pairs needs at the measured rates of its ops
+    model: ChaCha20 blocks (336 v_add_u32, 320 v_xor_b32, 320 v_alignbit_b32)
+    at the probe's rate for the real block, one per lane; a u64 MAC (one
+    v_mad_u64_u32, two v_mul_lo_u32, one v_add3_u32) at each instruction's."""
     r = {k: v * 1e12 for k, v in VALU_RATES_4W.items()}
-    chacha = 336 / r["add"] + 320 / r["xor"] + 320 / r["alignbit"]
+    chacha = CHACHA_BLOCK_OPS / r["chacha_block"]
     mac = 1 / r["mad_u64"] + 2 / r["mul_lo"] + 1 / r["add3"]
     return B * (leveled_blocks_per_pair(p, D) * chacha + p.k * p.N * D * mac)
 
