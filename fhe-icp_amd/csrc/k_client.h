@@ -311,9 +311,9 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 // exactly (mod 2^64), so
 //   b = <a, s> + sum_j w_j (x_j Delta + e_j) + cst Delta,
 // bit-identical to the two kernels. The features' noise blocks (ceil(Dg / 8)
-// of them) follow the mask blocks on threads 0.. (a fifth wave for them
-// measured 28 us per 1024 pairs against 26; rotating them over the waves by
-// pair, 28.7, docs/AB_LOG_r04.md). The key words of the thread's eight mask
+// of them) follow the mask blocks, each on the four lanes of a quad
+// (chacha20_block_quad: 300 instructions instead of a second 976-instruction
+// pass of a wave for two blocks at D = 16), spread over the four waves. The key words of the thread's eight mask
 // words are loaded at the start, behind the ChaCha20 work.
 // Phase stamps (tools/el_stamps.py): a launch of 1024 pairs puts exactly four
 // workgroups on every CU and one wave of each on every SIMD; the four run
@@ -366,16 +366,24 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
       for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
     }
     EL_STAMP(2, __builtin_amdgcn_s_memtime());
-    // the features' noise words, 8 per block
-    for (int blk = threadIdx.x; 8 * blk < Dg; blk += 256) {
-      u64 e[8];
-      stream_block(K, TAG_ENC_NOISE, id, (uint32_t)blk, e);
+    // the features' noise words, 8 per block, each block on a quad of lanes
+    // (chacha20_block_quad): noise block nb on quad nb / 4 of wave nb mod 4;
+    // the even lanes of the quad hold the low words of u64 words
+    // j = (q + 4 r) / 2, the odd ones the high words
+    {
+      const int q = (int)(threadIdx.x & 3), wv = (int)(threadIdx.x >> 6), qd = (int)((threadIdx.x & 63) >> 2);
+      for (int nb = 4 * qd + wv; 8 * nb < Dg; nb += 64) {
+        uint32_t e4[4];
+        chacha20_block_quad(K, (uint32_t)nb, TAG_ENC_NOISE, id, q, e4);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int t = 8 * blk + q;
-        if (t < Dg)
-          bpart += (u64)w[g * N + t] *
-                   (((u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits)) + (u64)tuniform(e[q], noise_bits));
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t hi = quad_mov<QP_XOR1>(e4[r]);
+          const int t = 8 * nb + ((q + 4 * r) >> 1);
+          if ((q & 1) == 0 && t < Dg) {
+            const u64 e = (u64)e4[r] | ((u64)hi << 32);
+            bpart += (u64)w[g * N + t] * (((u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits)) + (u64)tuniform(e, noise_bits));
+          }
+        }
       }
     }
     EL_STAMP(3, __builtin_amdgcn_s_memtime());

@@ -70,6 +70,41 @@ __host__ __device__ __forceinline__ void chacha20_block(const ChaKey& K, uint32_
 }
 #undef FHEI_QR
 
+// One ChaCha20 block computed by the four lanes of a quad (lane q = lane & 3
+// holds column q: state words q, 4 + q, 8 + q, 12 + q): the column round is
+// each lane's own quarter round, the diagonal round the same after rotating
+// rows 1-3 of the state by 1, 2, 3 lanes (DPP quad_perm, and back). 10 x (24
+// + 6) instructions per lane instead of 976 on one lane: for the few blocks a
+// workgroup needs beside a full pass (k_encrypt_linear's noise words). All
+// four lanes of the quad must be active. out[r] = output word q + 4 r.
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_mov(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+constexpr int QP_ROT1 = 0x39, QP_ROT2 = 0x4e, QP_ROT3 = 0x93, QP_XOR1 = 0xb1;  // quad_perm [1230] [2301] [3012] [1032]
+#define FHEI_QRL(a, b, c, d)                      \
+  a += b; d ^= a; d = rotl32(d, 16);              \
+  c += d; b ^= c; b = rotl32(b, 12);              \
+  a += b; d ^= a; d = rotl32(d, 8);               \
+  c += d; b ^= c; b = rotl32(b, 7);
+__device__ __forceinline__ void chacha20_block_quad(const ChaKey& K, uint32_t counter, uint32_t tag, uint64_t id,
+                                                    int q, uint32_t out[4]) {
+  const uint32_t a0 = q == 0 ? 0x61707865u : q == 1 ? 0x3320646eu : q == 2 ? 0x79622d32u : 0x6b206574u;
+  const uint32_t b0 = q == 0 ? K.w[0] : q == 1 ? K.w[1] : q == 2 ? K.w[2] : K.w[3];
+  const uint32_t c0 = q == 0 ? K.w[4] : q == 1 ? K.w[5] : q == 2 ? K.w[6] : K.w[7];
+  const uint32_t d0 = q == 0 ? counter : q == 1 ? tag : q == 2 ? (uint32_t)id : (uint32_t)(id >> 32);
+  uint32_t a = a0, b = b0, c = c0, d = d0;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    FHEI_QRL(a, b, c, d)
+    b = quad_mov<QP_ROT1>(b); c = quad_mov<QP_ROT2>(c); d = quad_mov<QP_ROT3>(d);
+    FHEI_QRL(a, b, c, d)
+    b = quad_mov<QP_ROT3>(b); c = quad_mov<QP_ROT2>(c); d = quad_mov<QP_ROT1>(d);
+  }
+  out[0] = a + a0; out[1] = b + b0; out[2] = c + c0; out[3] = d + d0;
+}
+#undef FHEI_QRL
+
 // Eight consecutive u64 words [8*blk, 8*blk+8) of stream (tag, id).
 __host__ __device__ __forceinline__ void stream_block(const ChaKey& K, uint32_t tag, uint64_t id, uint32_t blk,
                                                       uint64_t w[8]) {
