@@ -27,8 +27,9 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, unsigned seed) {
   unsigned x[8], y = seed ^ threadIdx.x;
   float f[8], g = (float)(threadIdx.x & 7) * 1e-3f;
   unsigned long long m[8];
+  double d[8], dg = 1.0 + 1e-9 * threadIdx.x, dh = 1e-3;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) x[c] = seed * (c + 1) + threadIdx.x, f[c] = (float)c, m[c] = x[c];
+  for (int c = 0; c < 8; ++c) x[c] = seed * (c + 1) + threadIdx.x, f[c] = (float)c, m[c] = x[c], d[c] = c;
   for (int i = 0; i < ITERS; ++i) {
 #define ADD(c) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
 #define XOR(c) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
@@ -37,6 +38,7 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, unsigned seed) {
 #define MUL(c) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[c]) : "v"(y));
 #define MAD(c) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(m[c]) : "v"(x[c]), "v"(y) : "vcc");
 #define AD3(c) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x[c]) : "v"(y));
+#define F64(c) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(d[c]) : "v"(dg), "v"(dh));
     if constexpr (OP == 0) { OP8(ADD) }
     if constexpr (OP == 1) { OP8(XOR) }
     if constexpr (OP == 2) { OP8(ALB) }
@@ -45,6 +47,7 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, unsigned seed) {
     if constexpr (OP == 5) { OP8(MAD) }
     if constexpr (OP == 6) { OP8(AD3) }
     if constexpr (OP == 7) { OP8(ADD) OP8(XOR) OP8(ALB) }  // ChaCha20's mix, 1:1:1
+    if constexpr (OP == 10) { OP8(F64) }
     if constexpr (OP >= 8) {  // the product's ChaCha20 block (976 ops), 1 or 2 per step
       if ((i & 7) == 0) {
         fhei::ChaKey K;
@@ -64,7 +67,8 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, unsigned seed) {
   }
   unsigned r = 0;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) r ^= x[c] ^ __float_as_uint(f[c]) ^ (unsigned)m[c] ^ (unsigned)(m[c] >> 32);
+  for (int c = 0; c < 8; ++c)
+    r ^= x[c] ^ __float_as_uint(f[c]) ^ (unsigned)m[c] ^ (unsigned)(m[c] >> 32) ^ (unsigned)__double_as_longlong(d[c]);
   out[blockIdx.x * 256 + threadIdx.x] = r;
 }
 
@@ -102,7 +106,8 @@ int main() {
         run<2>("v_alignbit_b32", 8, blocks, d) || run<3>("v_add_f32", 8, blocks, d) ||
         run<4>("v_mul_lo_u32", 8, blocks, d) || run<5>("v_mad_u64_u32", 8, blocks, d) ||
         run<6>("v_add3_u32", 8, blocks, d) || run<7>("add/xor/alignbit 1:1:1", 24, blocks, d) ||
-        run<8>("chacha20 x1 (976/8 per it)", 122, blocks, d) || run<9>("chacha20 x2 (976/4 per it)", 244, blocks, d))
+        run<8>("chacha20 x1 (976/8 per it)", 122, blocks, d) || run<9>("chacha20 x2 (976/4 per it)", 244, blocks, d) ||
+        run<10>("v_fma_f64", 8, blocks, d))
       return 1;
   }
   return 0;
