@@ -218,65 +218,6 @@ __device__ __forceinline__ void packed_mac8(const u64* A, int N, int u0, const i
   }
 }
 
-// The same sums on the f64 FMA pipe, for chunks whose weights are all below
-// 2^11 in magnitude (every quantized model: n_bits <= 12). Each mask word
-// splits into its halves, alo + 2^32 ahi, so
-//   sum_t w_t Ahat[t - u] = L + 2^32 H (mod 2^64),
-//   L = sum_t w_t alo_t,  H = sum_t w_t ahi_t,
-// and with at most N = 1024 features of |w| < 2^11, |L|, |H| < 2^53: every
-// partial sum is an integer the f64 FMA holds exactly. Per feature and lane:
-// one LDS read, two conversions and 16 v_fma_f64 (4 cycles each) against
-// eight u64 products of four VOP3 integer instructions (tools/valu_probe.hip).
-// Window: Ahat[m] lives in slot (m + u0) & 7 as its two halves in f64, one new
-// word per feature; feature j reads output r's word from slot (j - r) & 7.
-__device__ __forceinline__ u64 f64_exact_to_u64(double x) {  // |x| < 2^53, an integer
-  const double h = floor(x * 0x1p-32);
-  const double l = fma(h, -0x1p32, x);  // exact, in [0, 2^32)
-  return ((u64)(int64_t)(int)h << 32) + (u64)(uint32_t)l;
-}
-constexpr int64_t PACKED_F64_WMAX = 1 << 11;
-__device__ __forceinline__ void packed_mac8_f64(const u64* A, int N, int u0, const int64_t* __restrict__ w, int Dg,
-                                                u64 acc[8]) {
-  double wl[8], wh[8], lo[8], hi[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) lo[r] = hi[r] = 0.0;
-#pragma unroll
-  for (int d = 1; d < 8; ++d) {
-    const u64 v = ahat_w(A, -d - u0, N);
-    wl[8 - d] = (double)(uint32_t)v;
-    wh[8 - d] = (double)(uint32_t)(v >> 32);
-  }
-  wl[0] = wh[0] = 0.0;
-  int64_t wreg = 0;
-  const int lane = threadIdx.x & 63;
-  for (int j0 = 0; j0 < Dg; j0 += 8) {
-    if ((j0 & 63) == 0) {
-      const int jl = j0 + lane;
-      wreg = jl < Dg ? w[jl] : 0;  // 0 past Dg: those features weigh nothing
-    }
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const u64 v = ahat_w(A, j0 + jj - u0, N);
-      wl[jj] = (double)(uint32_t)v;
-      wh[jj] = (double)(uint32_t)(v >> 32);
-      const double wd = (double)__builtin_amdgcn_readlane((int)wreg, (j0 & 63) + jj);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        lo[r] = fma(wd, wl[(jj - r) & 7], lo[r]);
-        hi[r] = fma(wd, wh[(jj - r) & 7], hi[r]);
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 8; ++r) acc[r] += f64_exact_to_u64(lo[r]) + (f64_exact_to_u64(hi[r]) << 32);
-}
-// 1 when every weight of the chunk is below PACKED_F64_WMAX in magnitude
-__device__ __forceinline__ int packed_small_weights(const int64_t* __restrict__ wg, int Dg) {
-  int ok = 1;
-  for (int t = threadIdx.x; t < Dg; t += blockDim.x) ok &= (wg[t] > -PACKED_F64_WMAX) & (wg[t] < PACKED_F64_WMAX);
-  return ok;
-}
-
 // Client side: GLWE encryption of the packed features (fhe_encrypt_packed_batch).
 // One 256-thread workgroup per GLWE (pair b, chunk g); the body's negacyclic
 // products with the binary key run as in k_keygen_bsk. glwe: [B][G][(k+1)N].
@@ -323,16 +264,12 @@ __global__ void __launch_bounds__(256) k_encrypt_packed(ChaKey K, int N, int k, 
 // The per-pair extraction shared by the two kernels below: thread t owns mask
 // words [8t, 8t + 8) of the output LWE (component i = 8t / N), with A of the
 // chunk in LDS. Returns nothing; accumulates into acc.
-// small: every weight of the chunk below PACKED_F64_WMAX (workgroup-uniform).
 __device__ __forceinline__ void packed_chunk_mask(const u64* A, int N, int k, const int64_t* __restrict__ wg, int Dg,
-                                                  bool small, u64 acc[8]) {
+                                                  u64 acc[8]) {
   const int t8 = 8 * threadIdx.x;
   if (t8 < k * N) {
     const int i = t8 / N;
-    if (small)
-      packed_mac8_f64(A + (size_t)i * N, N, t8 - i * N, wg, Dg, acc);
-    else
-      packed_mac8(A + (size_t)i * N, N, t8 - i * N, wg, Dg, acc);
+    packed_mac8(A + (size_t)i * N, N, t8 - i * N, wg, Dg, acc);
   }
 }
 
@@ -353,8 +290,8 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
     __syncthreads();  // the previous chunk's readers are done
     for (int t = threadIdx.x; t < k * N; t += 256) shm[t] = in[t];
     for (int t = threadIdx.x; t < Dg; t += 256) bpart += (u64)w[g * N + t] * in[(size_t)k * N + t];
-    const bool small = __syncthreads_and(packed_small_weights(w + g * N, Dg));
-    packed_chunk_mask(shm, N, k, w + g * N, Dg, small, acc);
+    __syncthreads();
+    packed_chunk_mask(shm, N, k, w + g * N, Dg, acc);
   }
   const int t8 = 8 * threadIdx.x;
   u64* o = out + (size_t)b * (k * N + 1);
@@ -376,9 +313,8 @@ __global__ void __launch_bounds__(256) k_linear_packed(int N, int k, const u64* 
 // bit-identical to the two kernels. The features' noise blocks (ceil(Dg / 8)
 // of them) follow the mask blocks, each on the four lanes of a quad
 // (chacha20_block_quad: 300 instructions instead of a second 976-instruction
-// pass of a wave for two blocks at D = 16), spread over the four waves.
-// Four waves per SIMD (launch bounds: at most 128 VGPRs), so a 1024-pair launch
-// is one round of four workgroups per CU.
+// pass of a wave for two blocks at D = 16), spread over the four waves. The key words of the thread's eight mask
+// words are loaded at the start, behind the ChaCha20 work.
 // Phase stamps (tools/el_stamps.py): a launch of 1024 pairs puts exactly four
 // workgroups on every CU and one wave of each on every SIMD; the four run
 // 19k to 47k cycles as the SIMDs issue by wave age, so a CU's span is set by
@@ -403,7 +339,7 @@ __device__ unsigned long long g_el_stamps[1024][4][8];
   do {                 \
   } while (0)
 #endif
-__global__ void __launch_bounds__(EL_THREADS, 4) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
+__global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, int k, int msg_bits, int noise_bits,
                                                         const u64* __restrict__ s_big, const int64_t* __restrict__ x,
                                                         int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
                                                         u64 id0, u64* __restrict__ out) {
@@ -414,6 +350,9 @@ __global__ void __launch_bounds__(EL_THREADS, 4) k_encrypt_linear(ChaKey K, int 
   EL_STAMP(0, __builtin_amdgcn_s_memrealtime());
   EL_STAMP(1, __builtin_amdgcn_s_memtime());
   const int t8 = 8 * threadIdx.x;
+  u64 key[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) key[q] = t8 < k * N ? s_big[t8 + q] : 0;
   u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 bpart = 0;
   for (int g = 0; g < G; ++g) {
@@ -448,9 +387,9 @@ __global__ void __launch_bounds__(EL_THREADS, 4) k_encrypt_linear(ChaKey K, int 
       }
     }
     EL_STAMP(3, __builtin_amdgcn_s_memtime());
-    const bool small = __syncthreads_and(packed_small_weights(w + g * N, Dg));
+    __syncthreads();
     EL_STAMP(4, __builtin_amdgcn_s_memtime());
-    packed_chunk_mask(shm, N, k, w + g * N, Dg, small, acc);
+    packed_chunk_mask(shm, N, k, w + g * N, Dg, acc);
     EL_STAMP(5, __builtin_amdgcn_s_memtime());
   }
   u64* o = out + (size_t)b * (k * N + 1);
@@ -459,7 +398,7 @@ __global__ void __launch_bounds__(EL_THREADS, 4) k_encrypt_linear(ChaKey K, int 
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       o[t8 + q] = acc[q];
-      sdot += acc[q] & (0 - s_big[t8 + q]);
+      sdot += acc[q] & (0 - key[q]);
     }
   }
   const u64 tot = block_sum_u64<EL_THREADS>(sdot + bpart, red);

@@ -496,27 +496,16 @@ def test_encrypt_linear_fused_bit_exact(which, request):
     fhe_linear_packed_batch, and both to the oracle's textbook GLWE encryption
     + product + sample extraction; GLWEs equal the oracle's word for word. D
     covers a count that is not a multiple of anything (37), the compare
-    path's 16, and more features than N (two GLWEs per row). Weights below
-    2^11 take the f64-FMA MAC (packed_mac8_f64), others the u64 one: the
-    "edge" case puts N weights of magnitude 2047 in one chunk (its f64 sums at
-    the 2^53 bound), the "wide" case draws them over the whole int64 range;
-    both are checked word for word only (their messages wrap)."""
+    path's 16, and more features than N (two GLWEs per row); the last case
+    draws weights over the whole int64 range (the MAC's general high-word
+    term, |w| >= 2^31) and is checked word for word only (its message wraps)."""
     eng, ref = request.getfixturevalue(which)
     rng = np.random.default_rng(11)
     N = eng.params.N
-    for B, D, kind in ((5, 37, "q"), (64, 16, "q"), (3, N + 44, "q"), (4, 70, "wide"), (2, N, "edge"),
-                       (3, 40, "mixed")):
+    for B, D in ((5, 37), (64, 16), (3, N + 44), (4, 70)):
         x = rng.integers(-32, 32, (B, D))
-        wide = kind != "q"
-        if kind == "wide":
-            w = rng.integers(-2 ** 63, 2 ** 63 - 1, D)
-        elif kind == "edge":
-            w = np.where(rng.integers(0, 2, D) == 1, 2047, -2047)
-        elif kind == "mixed":  # one weight at the threshold sends the chunk to the u64 MAC
-            w = rng.integers(-127, 128, D)
-            w[7] = 2048
-        else:
-            w = rng.integers(-127, 128, D)
+        wide = D == 70
+        w = rng.integers(-2 ** 63, 2 ** 63 - 1, D) if wide else rng.integers(-127, 128, D)
         cst = int(rng.integers(-1000, 1000))
         fused = u64(eng.encrypt_linear(x, w, cst, seed=8, id0=77))
         glwe = eng.encrypt_packed(x, seed=8, id0=77)
