@@ -325,9 +325,9 @@ constexpr int EL_THREADS = 256;
 // A/B builds (FHEICP_AB): per wave of the first 1024 workgroups, {s_memrealtime
 // at start, s_memtime at start / after the mask blocks / after the noise blocks
 // / after the barrier / after the MAC loop / at the end, s_memrealtime at the
-// end} (tools/el_stamps.py, fhe_debug_el_stamps)
+// end, HW_ID, XCC_ID} (tools/el_stamps.py, fhe_debug_el_stamps)
 #ifdef FHEICP_AB
-__device__ unsigned long long g_el_stamps[1024][4][8];
+__device__ unsigned long long g_el_stamps[1024][4][10];
 #define EL_STAMP(k, t)                  \
   do {                                  \
     __builtin_amdgcn_sched_barrier(0);  \
@@ -406,10 +406,13 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
 #ifdef FHEICP_AB
   EL_STAMP(6, __builtin_amdgcn_s_memtime());
   EL_STAMP(7, __builtin_amdgcn_s_memrealtime());
-  if ((threadIdx.x & 63) < 8 && b < 1024) {
+  if ((threadIdx.x & 63) < 10 && b < 1024) {
     unsigned long long v = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) v = (int)(threadIdx.x & 63) == q ? st_[q] : v;
+    // HW_ID (wave, SIMD, CU, SE fields) and XCC_ID
+    v = (threadIdx.x & 63) == 8 ? (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) : v;
+    v = (threadIdx.x & 63) == 9 ? (unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) : v;
     g_el_stamps[b][threadIdx.x >> 6][threadIdx.x & 63] = v;
   }
 #endif

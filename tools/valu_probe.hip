@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, unsigned seed) {
     if constexpr (OP == 6) { OP8(AD3) }
     if constexpr (OP == 7) { OP8(ADD) OP8(XOR) OP8(ALB) }  // ChaCha20's mix, 1:1:1
     if constexpr (OP == 10) { OP8(F64) }
-    if constexpr (OP >= 8) {  // the product's ChaCha20 block (976 ops), 1 or 2 per step
+    if constexpr (OP == 8 || OP == 9) {  // the product's ChaCha20 block (976 ops), 1 or 2 per step
       if ((i & 7) == 0) {
         fhei::ChaKey K;
 #pragma unroll
