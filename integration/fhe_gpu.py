@@ -39,6 +39,7 @@ _PROTOS = {
     "fhe_memcpy_d2h": (C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp]),
     "fhe_compare_batch": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     "fhe_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "fhe_score_batch": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp]),
 }
 
 
@@ -91,6 +92,24 @@ class GpuCompare:
                                               self.next_id, bufs[2], bufs[3], None))
             self.next_id += B * D
             return self._to_host(bufs[2], B), self._to_host(bufs[3], B)
+        finally:
+            for d in bufs:
+                self.L.fhe_dev_free(self.ctx, d)
+
+    def score(self, q_x: np.ndarray, q_w: np.ndarray, cst: int, centre: int):
+        """The reference's own encrypted predict (fhe_similarity.py:151,
+        predict(fhe="execute")): packed encryption + leveled dot + decryption,
+        no bootstrap; the accumulators int64[B] (dequantize on the host).
+        centre: the middle of the accumulator range, (lo + hi) // 2, so that
+        acc - centre fits the msg_bits encoding."""
+        q_x = np.asarray(q_x, np.int64)
+        B, D = q_x.shape
+        bufs = [self._to_dev(q_x), self._to_dev(np.asarray(q_w, np.int64)), self._alloc(8 * B)]
+        try:
+            self._ok(self.L.fhe_score_batch(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(centre), self.enc_seed,
+                                            self.next_id, bufs[2], None))
+            self.next_id += B * D
+            return self._to_host(bufs[2], B)
         finally:
             for d in bufs:
                 self.L.fhe_dev_free(self.ctx, d)

@@ -134,10 +134,12 @@ def test_reference_side_ctypes_binding(need_gpu):
     eng = GpuCompare(params_for_bits(P).as_dict(), key_seed=99, lib_path=str(LIB_PATH))
     try:
         acc, below = eng.compare(qx, ref.q_w, ref.const_term, T)
+        scored = eng.score(qx, ref.q_w, ref.const_term, (lo + hi) // 2)
     finally:
         eng.close()
     np.testing.assert_array_equal(acc, acc_ref)
     np.testing.assert_array_equal(below, (acc_ref < T).astype(np.int64))
+    np.testing.assert_array_equal(scored, acc_ref)
 
 
 def test_key_manager_generate_load_and_processor(need_gpu, tmp_path):
