@@ -808,16 +808,6 @@ int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_enc, (hipStream_t)stream, &e1);
   ctx->prof_enc.kernel = "k_encrypt_linear";
-#if FHEICP_EL_SPLIT
-  if (p.N == 1024 && p.k <= 4 && B <= EL_SPLIT_MAX) {
-    hipLaunchKernelGGL(k_encrypt_linear_c, dim3((unsigned)(B * p.k)), dim3(128), (size_t)p.N * 8, (hipStream_t)stream, K,
-                       p.N, p.k, p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, d_w,
-                       ((u64)cst) << (64 - p.msg_bits), id0, d_out);
-    prof_end(ctx, ctx->prof_enc, (hipStream_t)stream, e1, B);
-    HIPCHK(ctx, hipGetLastError());
-    return FHE_OK;
-  }
-#endif
   hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(EL_THREADS), (size_t)p.k * p.N * 8, (hipStream_t)stream, K, p.N,
                      p.k, p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, d_w,
                      ((u64)cst) << (64 - p.msg_bits), id0, d_out);

@@ -418,82 +418,6 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
 #endif
 }
 
-#ifndef FHEICP_EL_SPLIT
-#define FHEICP_EL_SPLIT 0
-#endif
-#if FHEICP_EL_SPLIT
-// A/B builds only: k_encrypt_linear split by GLWE component, one 128-thread
-// workgroup per (pair, component i < k) generating only A_i (N / 8 ChaCha20
-// blocks) and extracting only its N outputs; component 0's workgroup also
-// runs the noise blocks. The body <a, s> + sum_j w_j (x_j Delta + e_j) + cst
-// Delta is summed from the k partials by the last workgroup of the pair to
-// arrive (per-pair counters, self-resetting; B <= EL_SPLIT_MAX).
-constexpr int EL_SPLIT_MAX = 1 << 16;
-__device__ u64 g_el_part[EL_SPLIT_MAX * 4];
-__device__ unsigned int g_el_cnt[EL_SPLIT_MAX];
-__global__ void __launch_bounds__(128) k_encrypt_linear_c(ChaKey K, int N, int k, int msg_bits, int noise_bits,
-                                                         const u64* __restrict__ s_big, const int64_t* __restrict__ x,
-                                                         int D, int G, const int64_t* __restrict__ w, u64 cst_scaled,
-                                                         u64 id0, u64* __restrict__ out) {
-  extern __shared__ u64 shm[];
-  __shared__ u64 red[2];
-  const int64_t b = blockIdx.x / k;
-  const int i = (int)(blockIdx.x - b * k);
-  const int t = threadIdx.x, t8 = 8 * t;  // N / 8 = 128 threads
-  u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  u64 bpart = 0;
-  for (int g = 0; g < G; ++g) {
-    const u64 id = id0 + (u64)b * G + g;
-    const int Dg = min(D - g * N, N);
-    __syncthreads();
-    {
-      u64 m[8];
-      stream_block(K, TAG_ENC_MASK, id, (uint32_t)(i * N / 8 + t), m);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) shm[t8 + q] = m[q];
-    }
-    if (i == 0) {
-      const int q = t & 3, wv = t >> 6, qd = (t & 63) >> 2;
-      for (int nb = 2 * qd + wv; 8 * nb < Dg; nb += 32) {
-        uint32_t e4[4];
-        chacha20_block_quad(K, (uint32_t)nb, TAG_ENC_NOISE, id, q, e4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t hi = quad_mov<QP_XOR1>(e4[r]);
-          const int tt = 8 * nb + ((q + 4 * r) >> 1);
-          if ((q & 1) == 0 && tt < Dg) {
-            const u64 e = (u64)e4[r] | ((u64)hi << 32);
-            bpart += (u64)w[g * N + tt] * (((u64)x[(size_t)b * D + g * N + tt] << (64 - msg_bits)) + (u64)tuniform(e, noise_bits));
-          }
-        }
-      }
-    }
-    __syncthreads();
-    packed_mac8(shm, N, t8, w + g * N, Dg, acc);
-  }
-  u64* o = out + (size_t)b * (k * N + 1) + (size_t)i * N;
-  u64 sdot = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    o[t8 + q] = acc[q];
-    sdot += acc[q] & (0 - s_big[(size_t)i * N + t8 + q]);
-  }
-  const u64 tot = block_sum_u64<128>(sdot + bpart, red);
-  if (t == 0) {
-    __hip_atomic_store(&g_el_part[b * k + i], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
-    const unsigned int old = atomicAdd(&g_el_cnt[b], 1u);
-    if (old == (unsigned)(k - 1)) {
-      __threadfence();
-      u64 sum = 0;
-      for (int j = 0; j < k; ++j) sum += __hip_atomic_load(&g_el_part[b * k + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      out[(size_t)b * (k * N + 1) + (size_t)k * N] = sum + cst_scaled;
-      atomicExch(&g_el_cnt[b], 0u);
-    }
-  }
-}
-#endif
-
 // A seeded LWE keeps only its body; the mask is stream(TAG_ENC_MASK, id) of
 // a PUBLIC mask key Km, the noise stream(TAG_ENC_NOISE, id) of a SECRET
 // noise key Kn. Document b of a corpus holds D bodies,
