@@ -7,12 +7,15 @@ against 1024 documents, 16-dim features, n_bits = 6. At N > 1 (or with
 search, 16-dim, n_bits = 6, the corpus sharded over the ranks in contiguous
 global index ranges (strong scaling: the total is fixed). One step = one pass
 of the whole encrypted path over each rank's shard, all on the GPU:
-    pair features + quantize -> encrypt (D LWEs per pair) -> leveled dot
-    product with the quantized weights -> decrypt the accumulator ->
-    P-round exact bit extraction (P key switches + P bootstraps per pair)
+    pair features + quantize -> packed GLWE encryption of the features fused
+    with the leveled dot product (one GLWE mask per pair, k_encrypt_linear)
+    -> decrypt the accumulator -> exact sign extraction of acc - T in 4-bit
+    digits (fhe_sign_pbs_count key switches + bootstraps per pair: 7 at
+    P = 16, on the multi-bit (15,2) and (23,1) rotations)
     -> decrypt the encrypted threshold bit -> local top-k
-and, for N > 1, the RCCL all-gather of the per-shard top-k (the only
-exchange step of the sharded search) plus the merge.
+and, whenever a process group exists (any launcher run, N = 1 included), the
+RCCL all-gather of the per-shard top-k (the only exchange step of the sharded
+search) plus the merge.
 Inputs (query, documents) are resident in HBM before the timed region.
 value = compares processed by all ranks / (max over ranks of the time).
 
@@ -124,16 +127,26 @@ def launch_ranks(args, argv: list[str]) -> int | None:
     return child.wait()
 
 
+def dist_on() -> bool:
+    """A process group exists: every collective of the run keys on this, not
+    on world > 1, so a one-rank launcher run executes the RCCL path too."""
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
 def dist_setup(args):
+    """Under a launcher (WORLD_SIZE set, any size, 1 included) this joins the
+    process group, RCCL (backend "nccl") bound to this rank's GPU unless
+    FHEICP_DIST_BACKEND says otherwise; run bare at N = 1 it creates none."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # one process per GPU; FHEICP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
         backend = os.environ.get("FHEICP_DIST_BACKEND", "nccl")
         local = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -404,21 +417,21 @@ def main():
     torch.cuda.synchronize()
 
     eng.profile(True)
-    if world > 1:
+    if dist_on():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         acc, below, oa, oi = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     eng.profile(False)
     br = read_br(eng)
     ks = eng.profile_read("keyswitch")
 
-    if world > 1:
+    if dist_on():
         on_dev = torch.distributed.get_backend() == "nccl"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if on_dev else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -432,7 +445,7 @@ def main():
     # every rank checks its own shard against the clear restatement of the
     # reference path; the flags meet in one all-reduce (MIN)
     par = shard_parity(args, model, q_np, docs_np, acc, below, T)
-    if world > 1:
+    if dist_on():
         flags = torch.tensor([int(par["acc_bit_exact"]), int(par["threshold_bit_exact"]),
                               int(par["quant_params_equal"]), par["compares_checked"]], dtype=torch.int64)
         on_dev = torch.distributed.get_backend() == "nccl"
@@ -462,7 +475,7 @@ def main():
                          if args.workload == "c4" else f"batch compare 1 query x {B} encrypted docs per GPU")
                         + f", {args.dim}-dim, n_bits={args.n_bits}"
                         f"{config_tag(args)} + encrypted threshold (min_similarity {args.min_similarity}) "
-                        f"+ top-{args.top_k}" + (" + RCCL top-k all-gather" if world > 1 else ""),
+                        f"+ top-{args.top_k}" + (" + RCCL top-k all-gather" if dist_on() else ""),
             "docs_per_gpu": B, "total_docs": args.total_docs if args.workload == "c4" else world * B,
             "dim": args.dim, "n_bits": args.n_bits, "msg_bits_P": P,
             "pbs_per_compare": n_pbs, "keyswitch_per_compare": n_pbs,
@@ -475,19 +488,42 @@ def main():
 
     out["parity"] = par
     out["leveled_score"] = leveled_score(args, model, q_dev, d_dev, acc)
-    if world > 1:
+    if dist_on():
         out["allgather_ms"] = round(allgather_ms, 4)
-    else:
+        out["dist"] = dist_info(dev)
+    if world == 1:
         out["pcie_inclusive"] = pcie_inclusive(args, model, q_dev, docs_np, T, dev)
     if rank == 0:
         out["topk_check"] = topk_check(args, model, world, oa, oi)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_leg(args, model, q_np, docs_np, par)
 
+    share_note(out, world)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on():
         torch.distributed.destroy_process_group()
+
+
+def dist_info(dev) -> dict:
+    """What ran the collectives: the backend and, for RCCL, the device it is
+    bound to."""
+    b = torch.distributed.get_backend()
+    return {"backend": b, "rccl": b == "nccl", "world_size": torch.distributed.get_world_size(),
+            "device": str(dev) if b == "nccl" else "cpu (host copies)"}
+
+
+def share_note(out: dict, world: int) -> None:
+    """Ranks sharing GPUs (a gloo rehearsal of N ranks on fewer cards): the
+    per-launch kernel times include the other ranks' kernels, so the roofline
+    is not a per-GPU figure; the line says so and carries it only as raw."""
+    ngpu = torch.cuda.device_count()
+    if world > ngpu:
+        note = f"{world} ranks share {ngpu} GPU(s): kernel launch times overlap other ranks' kernels"
+        out["config"]["gpu_sharing"] = note
+        raw = out.pop("roofline", None)
+        out["roofline"] = {"per_gpu": False, "note": note + "; the fraction below is not a per-GPU roofline",
+                           "shared_raw": raw}
 
 
 VALU_PEAK_TOPS = 78.6   # 32-bit VALU lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
@@ -747,20 +783,20 @@ def corpus_main(args, world, rank, local, dev):
         step()
     torch.cuda.synchronize()
     eng.profile(True)
-    if world > 1:
+    if dist_on():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         acc, below, oa, oi = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     eng.profile(False)
     br = read_br(eng)
     ks = eng.profile_read("keyswitch")
-    if world > 1:
+    if dist_on():
         on_dev = torch.distributed.get_backend() == "nccl"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if on_dev else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -802,7 +838,7 @@ def corpus_main(args, world, rank, local, dev):
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = corpus_cpu_leg(args, c, bodies, ids, oq, cq, q_np, docs_np, P, out["parity"])
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on():
         torch.distributed.destroy_process_group()
 
 
@@ -868,19 +904,19 @@ def embed_main(args, world, rank, local, dev):
         g.forward(ids_d, mask_d)
     torch.cuda.synchronize()
     g.profile(True)
-    if world > 1:
+    if dist_on():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = g.forward(ids_d, mask_d)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     g.profile(False)
     prof = {k: g.profile_read(k) for k in ("gemm", "attention", "other")}
-    if world > 1:
+    if dist_on():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -952,7 +988,7 @@ def embed_main(args, world, rank, local, dev):
                                               f"bert_embeddings.py:136), {cores} threads"}
     if rank == 0:
         print(json.dumps(out_line), flush=True)
-    if world > 1:
+    if dist_on():
         torch.distributed.destroy_process_group()
 
 

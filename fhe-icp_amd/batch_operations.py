@@ -403,7 +403,12 @@ class BatchProcessor:
         vectors that meet in one score come from one reducer and one encoder.
         A GPU stage is not bit-equal to the CPU one it replaces, and a feature
         on the other side of an input-quantizer rounding boundary changes the
-        accumulator; within one provenance every score is the oracle's."""
+        accumulator; within one provenance every score is the oracle's.
+        An untagged vector counts as the CPU stage (torch fp32 encoder, sklearn
+        PCA). Stores written before round 4 are the exception: a BertEmbedder
+        on a GPU then ran the HIP bf16 encoder without tagging, so vectors such
+        a store holds have unknown encoder provenance (re-embed them, or accept
+        the mix explicitly with allow_mixed_embedders)."""
         what = ((REDUCER_KEY, "dimension reducers", "the GPU and CPU PCA", "gpu_reducer", "allow_mixed_reducers"),
                 (EMBEDDER_KEY, "embedders", "the HIP and torch BERT encoders", "gpu_embedder",
                  "allow_mixed_embedders"))

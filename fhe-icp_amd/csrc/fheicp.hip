@@ -747,25 +747,43 @@ int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s
   return FHE_OK;
 }
 
-int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_t seed, uint64_t id0,
-                      uint64_t* d_ct, void* stream) {
+// The encryption entry points take the stream key either as 32 bytes
+// (fhe_*_key: the product, a fresh CSPRNG key per session) or as a 64-bit
+// seed expanded by splitmix64 (reproducible tests and benches only).
+static bool key_arg(const uint32_t* h_key, ChaKey& K) {
+  if (!h_key) return false;
+  memcpy(K.w, h_key, 32);
+  return true;
+}
+
+static int encrypt_impl(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, const ChaKey& K, uint64_t id0,
+                        uint64_t* d_ct, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (count < 0 || (count > 0 && (!d_msg || !d_ct))) return fail(ctx, FHE_E_ARG, "bad encrypt arguments");
   if (count == 0) return FHE_OK;
   const fhe_params& p = ctx->p;
-  ChaKey K = key_from_seed(seed);
   hipLaunchKernelGGL(k_encrypt, dim3((unsigned)count), dim3(256), 0, (hipStream_t)stream, K, p.k * p.N, p.msg_bits,
                      p.glwe_noise_bits, ctx->s_big, d_msg, id0, d_ct);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
+int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_t seed, uint64_t id0,
+                      uint64_t* d_ct, void* stream) {
+  return encrypt_impl(ctx, d_msg, count, key_from_seed(seed), id0, d_ct, stream);
+}
+int fhe_encrypt_batch_key(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, const uint32_t h_key[8], uint64_t id0,
+                          uint64_t* d_ct, void* stream) {
+  ChaKey K;
+  if (!key_arg(h_key, K)) return fail(ctx, FHE_E_ARG, "null encryption key");
+  return encrypt_impl(ctx, d_msg, count, K, id0, d_ct, stream);
+}
 
 // GLWEs per pair of the packed feature encoding (k_client.h)
 static int packed_chunks(const fhe_params& p, int32_t D) { return (D + p.N - 1) / p.N; }
 
-int fhe_encrypt_packed_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
-                             uint64_t* d_glwe, void* stream) {
+static int encrypt_packed_impl(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const ChaKey& K,
+                               uint64_t id0, uint64_t* d_glwe, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_glwe))) return fail(ctx, FHE_E_ARG, "bad packed-encrypt arguments");
@@ -773,12 +791,21 @@ int fhe_encrypt_packed_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32
   const fhe_params& p = ctx->p;
   const int G = packed_chunks(p, D);
   if (B * G > 0x7fffffffLL) return fail(ctx, FHE_E_ARG, "packed-encrypt batch too large: split the call");
-  const ChaKey K = key_from_seed(seed);
   const size_t lds = (size_t)p.k * p.N * 9;
   hipLaunchKernelGGL(k_encrypt_packed, dim3((unsigned)(B * G)), dim3(256), lds, (hipStream_t)stream, K, p.N, p.k,
                      p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, id0, d_glwe);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
+}
+int fhe_encrypt_packed_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
+                             uint64_t* d_glwe, void* stream) {
+  return encrypt_packed_impl(ctx, d_qx, B, D, key_from_seed(seed), id0, d_glwe, stream);
+}
+int fhe_encrypt_packed_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const uint32_t h_key[8],
+                                 uint64_t id0, uint64_t* d_glwe, void* stream) {
+  ChaKey K;
+  if (!key_arg(h_key, K)) return fail(ctx, FHE_E_ARG, "null encryption key");
+  return encrypt_packed_impl(ctx, d_qx, B, D, K, id0, d_glwe, stream);
 }
 
 int fhe_linear_packed_batch(fhe_ctx* ctx, const uint64_t* d_glwe, int64_t B, int32_t D, const int64_t* d_w,
@@ -795,8 +822,8 @@ int fhe_linear_packed_batch(fhe_ctx* ctx, const uint64_t* d_glwe, int64_t B, int
   return FHE_OK;
 }
 
-int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
-                             const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream) {
+static int encrypt_linear_impl(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const ChaKey& K,
+                               uint64_t id0, const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_out))) return fail(ctx, FHE_E_ARG, "bad encrypt-linear arguments");
@@ -804,7 +831,6 @@ int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32
   const fhe_params& p = ctx->p;
   const int G = packed_chunks(p, D);
   if (B > 0x7fffffffLL || B * G > 0x7fffffffffffLL) return fail(ctx, FHE_E_ARG, "encrypt-linear batch too large: split the call");
-  const ChaKey K = key_from_seed(seed);
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_enc, (hipStream_t)stream, &e1);
   ctx->prof_enc.kernel = "k_encrypt_linear";
@@ -814,6 +840,16 @@ int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32
   prof_end(ctx, ctx->prof_enc, (hipStream_t)stream, e1, B);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
+}
+int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
+                             const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream) {
+  return encrypt_linear_impl(ctx, d_qx, B, D, key_from_seed(seed), id0, d_w, cst, d_out, stream);
+}
+int fhe_encrypt_linear_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const uint32_t h_key[8],
+                                 uint64_t id0, const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream) {
+  ChaKey K;
+  if (!key_arg(h_key, K)) return fail(ctx, FHE_E_ARG, "null encryption key");
+  return encrypt_linear_impl(ctx, d_qx, B, D, K, id0, d_w, cst, d_out, stream);
 }
 
 static int seeded_args(fhe_ctx* ctx, int64_t B, int32_t D, const void* a, const void* b, const void* c) {
@@ -1497,8 +1533,8 @@ int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_
   return bit_extract(ctx, d_ct_v, count, d_refreshed, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream);
 }
 
-int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
-                      int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream) {
+static int compare_impl(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                        int64_t T, const ChaKey& K, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_acc || !d_below)))
@@ -1516,7 +1552,7 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   u64* sgn = ctv + (size_t)B * Wb;
   u64* small = sgn + (size_t)B * Wb;
   int64_t* v = (int64_t*)(small + (size_t)B * Ws);
-  rc = fhe_encrypt_linear_batch(ctx, d_qx, B, D, enc_seed, id0, d_w, cst - T, ctv, stream);
+  rc = encrypt_linear_impl(ctx, d_qx, B, D, K, id0, d_w, cst - T, ctv, stream);
   if (rc) return rc;
   // The score comes from the leveled accumulator ciphertext (noise ~2^20,
   // as in the reference's leveled Concrete circuit); the PBS chain then
@@ -1531,12 +1567,23 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
 }
+int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                      int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream) {
+  return compare_impl(ctx, d_qx, B, D, d_w, cst, T, key_from_seed(enc_seed), id0, d_acc, d_below, stream);
+}
+int fhe_compare_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                          int64_t T, const uint32_t h_enc_key[8], uint64_t id0, int64_t* d_acc, int64_t* d_below,
+                          void* stream) {
+  ChaKey K;
+  if (!key_arg(h_enc_key, K)) return fail(ctx, FHE_E_ARG, "null encryption key");
+  return compare_impl(ctx, d_qx, B, D, d_w, cst, T, K, id0, d_acc, d_below, stream);
+}
 
 // The reference's own encrypted predict (fhe_similarity.py:142-160): the
 // leveled circuit only. No key switch and no bootstrap; T only centres the
 // accumulator in the msg_bits-bit encoding (acc - T must fit it).
-int fhe_score_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
-                    int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, void* stream) {
+static int score_impl(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                      int64_t T, const ChaKey& K, uint64_t id0, int64_t* d_acc, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (B < 0 || D <= 0 || (B > 0 && (!d_qx || !d_w || !d_acc))) return fail(ctx, FHE_E_ARG, "bad score arguments");
@@ -1549,13 +1596,23 @@ int fhe_score_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, con
   if (rc) return rc;
   u64* ctv = (u64*)ctx->ws;
   int64_t* v = (int64_t*)(ctv + (size_t)B * Wb);
-  rc = fhe_encrypt_linear_batch(ctx, d_qx, B, D, enc_seed, id0, d_w, cst - T, ctv, stream);
+  rc = encrypt_linear_impl(ctx, d_qx, B, D, K, id0, d_w, cst - T, ctv, stream);
   if (rc) return rc;
   rc = fhe_decrypt_batch(ctx, ctv, B, v, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(k_add_scalar, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, v, B, T, d_acc);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;
+}
+int fhe_score_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                    int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, void* stream) {
+  return score_impl(ctx, d_qx, B, D, d_w, cst, T, key_from_seed(enc_seed), id0, d_acc, stream);
+}
+int fhe_score_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                        int64_t T, const uint32_t h_enc_key[8], uint64_t id0, int64_t* d_acc, void* stream) {
+  ChaKey K;
+  if (!key_arg(h_enc_key, K)) return fail(ctx, FHE_E_ARG, "null encryption key");
+  return score_impl(ctx, d_qx, B, D, d_w, cst, T, K, id0, d_acc, stream);
 }
 
 int fhe_compare_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
@@ -1754,11 +1811,17 @@ int fhe_debug_el_stamps(fhe_ctx* ctx, uint64_t* h_out) {
 #endif
 }
 
+// FHEICP_SRC_SHA: sha256 (first 16 hex digits) of the sources the library was
+// compiled from, passed by __graft_entry__.build_lib (tests/test_abi.py checks
+// it against the tree, so a stale binary cannot pass for the current one)
+#ifndef FHEICP_SRC_SHA
+#define FHEICP_SRC_SHA "unknown"
+#endif
 const char* fhe_build_info(void) {
 #ifdef FHEICP_AB
-  return "libfheicp gfx950 ab=1";
+  return "libfheicp gfx950 ab=1 src=" FHEICP_SRC_SHA;
 #else
-  return "libfheicp gfx950 ab=0";
+  return "libfheicp gfx950 ab=0 src=" FHEICP_SRC_SHA;
 #endif
 }
 

@@ -185,8 +185,8 @@ __device__ __forceinline__ u64 readlane64(u64 v, int lane) {
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
 }
 // Weights: lane l of the wave holds w[64 c + l] of the current 64-feature
-// block c (one coalesced load per 64 features; whole waves call this: kN / 8
-// threads is a multiple of 64) and feature j's weight is broadcast by
+// block c (one coalesced load per 64 features; whole waves call this, all 64
+// lanes active: packed_chunk_mask) and feature j's weight is broadcast by
 // v_readlane into scalar registers, so the MAC loop touches no memory but the
 // window's LDS reads (a clamped global load per feature instead: 38 us per
 // 1024 pairs against 26, docs/AB_LOG_r04.md). The u64 product is the
@@ -264,12 +264,17 @@ __global__ void __launch_bounds__(256) k_encrypt_packed(ChaKey K, int N, int k, 
 // The per-pair extraction shared by the two kernels below: thread t owns mask
 // words [8t, 8t + 8) of the output LWE (component i = 8t / N), with A of the
 // chunk in LDS. Returns nothing; accumulates into acc.
+// packed_mac8 broadcasts the weights by v_readlane from every lane of the
+// wave, so the condition is per wave: a wave with any owned word runs it on
+// all 64 lanes (kN = 256 leaves lanes 32-63 of wave 0 without words); the
+// lanes past kN work on a clamped position and their acc is never stored.
 __device__ __forceinline__ void packed_chunk_mask(const u64* A, int N, int k, const int64_t* __restrict__ wg, int Dg,
                                                   u64 acc[8]) {
   const int t8 = 8 * threadIdx.x;
-  if (t8 < k * N) {
-    const int i = t8 / N;
-    packed_mac8(A + (size_t)i * N, N, t8 - i * N, wg, Dg, acc);
+  if (8 * (int)(threadIdx.x & ~63u) < k * N) {
+    const int tc = min(t8, k * N - 8);
+    const int i = tc / N;
+    packed_mac8(A + (size_t)i * N, N, tc - i * N, wg, Dg, acc);
   }
 }
 

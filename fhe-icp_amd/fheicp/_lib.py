@@ -55,12 +55,15 @@ SIGNATURES = [
     ("fhe_import_keys", C.c_int, [_CTXP, _vp, _vp, _vp, _vp]),
     ("fhe_export_fast_bsk", C.c_int, [_CTXP, _i32, _vp]),
     ("fhe_encrypt_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _vp, _vp]),
+    ("fhe_encrypt_batch_key", C.c_int, [_CTXP, _vp, _i64, _vp, _u64, _vp, _vp]),
     ("fhe_decrypt_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_decrypt_bits_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_phase_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _vp]),
     ("fhe_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     ("fhe_encrypt_linear_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _u64, _vp, _i64, _vp, _vp]),
+    ("fhe_encrypt_linear_batch_key", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _u64, _vp, _i64, _vp, _vp]),
     ("fhe_encrypt_packed_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _u64, _vp, _vp]),
+    ("fhe_encrypt_packed_batch_key", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _u64, _vp, _vp]),
     ("fhe_linear_packed_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     ("fhe_keyswitch_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _u64, _vp, _vp]),
     ("fhe_pbs_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _vp, _vp]),
@@ -76,7 +79,9 @@ SIGNATURES = [
     ("fhe_pbs_table_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _i32, _vp, _vp]),
     ("fhe_threshold_batch", C.c_int, [_CTXP, _vp, _i64, _i64, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
+    ("fhe_compare_batch_key", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _u64, _vp, _vp, _vp]),
     ("fhe_score_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp]),
+    ("fhe_score_batch_key", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _u64, _vp, _vp]),
     ("fhe_encrypt_seeded_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("fhe_expand_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     ("fhe_linear_seeded_batch", C.c_int, [_CTXP, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp, _vp]),

@@ -173,7 +173,11 @@ class EncryptedCorpus:
         if keys is not None:
             self.engine.import_keys(keys)
         else:
-            self.engine.keygen(int.from_bytes(os.urandom(8), "little") if key_seed is None else int(key_seed))
+            # 256-bit key from the OS CSPRNG; a key_seed is the 64-bit test form
+            if key_seed is None:
+                self.engine.keygen(key=os.urandom(32))
+            else:
+                self.engine.keygen(seed=int(key_seed))
         self.mask_key = (np.frombuffer(os.urandom(32), np.uint32).copy() if mask_key is None
                          else np.ascontiguousarray(mask_key, dtype=np.uint32).copy())
         self._noise_key = (np.frombuffer(os.urandom(32), np.uint32).copy() if noise_seed is None

@@ -69,9 +69,17 @@ class Engine:
         return self.params.msg_bits
 
     # ---------------------------------------------------------------- keys --
-    def keygen(self, seed: int) -> None:
+    def keygen(self, seed: int | None = None, key=None) -> None:
+        """Generate the keys from a 256-bit ChaCha20 key (8 u32 words or 32
+        bytes; fhe_keygen_key), or from a 64-bit seed (fhe_keygen: 64 bits of
+        entropy, reproducible tests and benches only). Exactly one is given."""
+        if (seed is None) == (key is None):
+            raise ValueError("keygen takes either a 64-bit seed or a 256-bit key")
         with torch.cuda.device(self.device):
-            self._chk(self._L.fhe_keygen(self._ctx, C.c_uint64(seed), _stream(self.device)))
+            if key is not None:
+                self._chk(self._L.fhe_keygen_key(self._ctx, self._key(key), _stream(self.device)))
+            else:
+                self._chk(self._L.fhe_keygen(self._ctx, C.c_uint64(seed), _stream(self.device)))
         self.has_keys = True
 
     def export_keys(self) -> dict:
@@ -151,14 +159,20 @@ class Engine:
                                            _stream(self.device)))
         return out
 
-    def encrypt_linear(self, msg, w, cst: int, seed: int, id0: int = 0) -> torch.Tensor:
-        """Fused encrypt + linear (fhe_encrypt_linear_batch): msg B x D ints."""
+    def encrypt_linear(self, msg, w, cst: int, seed, id0: int = 0) -> torch.Tensor:
+        """Fused encrypt + linear (fhe_encrypt_linear_batch[_key]): msg B x D
+        ints; `seed` is an int seed (tests) or a 256-bit stream key."""
         m = self.to_dev(msg)
         B, D = m.shape
         wd = self.to_dev(w)
         out = self.empty_big(B)
-        self._chk(self._L.fhe_encrypt_linear_batch(self._ctx, _ptr(m), B, D, C.c_uint64(seed), C.c_uint64(id0),
-                                                   _ptr(wd), int(cst), _ptr(out), _stream(self.device)))
+        if isinstance(seed, (int, np.integer)):
+            rc = self._L.fhe_encrypt_linear_batch(self._ctx, _ptr(m), B, D, C.c_uint64(int(seed)), C.c_uint64(id0),
+                                                  _ptr(wd), int(cst), _ptr(out), _stream(self.device))
+        else:
+            rc = self._L.fhe_encrypt_linear_batch_key(self._ctx, _ptr(m), B, D, self._key(seed), C.c_uint64(id0),
+                                                      _ptr(wd), int(cst), _ptr(out), _stream(self.device))
+        self._chk(rc)
         return out
 
     def encrypt_packed(self, msg, seed: int, id0: int = 0) -> torch.Tensor:
@@ -244,26 +258,37 @@ class Engine:
                                                 _stream(self.device)))
         return ref, sign
 
-    def compare(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc_seed: int, id0: int = 0):
+    def compare(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc, id0: int = 0):
         """Fused encrypt -> linear -> decrypt + sign extraction for B pairs.
+        `enc` is the session's 256-bit stream key (8 u32 words or 32 bytes:
+        fhe_compare_batch_key) or an int seed (fhe_compare_batch, tests).
 
         Returns (acc int64[B], below int64[B])."""
         B, D = q_x.shape
         acc = torch.empty(B, dtype=torch.int64, device=self.device)
         below = torch.empty(B, dtype=torch.int64, device=self.device)
-        self._chk(self._L.fhe_compare_batch(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T),
-                                            C.c_uint64(enc_seed), C.c_uint64(id0), _ptr(acc), _ptr(below),
-                                            _stream(self.device)))
+        if isinstance(enc, (int, np.integer)):
+            rc = self._L.fhe_compare_batch(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T), C.c_uint64(int(enc)),
+                                           C.c_uint64(id0), _ptr(acc), _ptr(below), _stream(self.device))
+        else:
+            rc = self._L.fhe_compare_batch_key(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T), self._key(enc),
+                                               C.c_uint64(id0), _ptr(acc), _ptr(below), _stream(self.device))
+        self._chk(rc)
         return acc, below
 
-    def score(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc_seed: int, id0: int = 0):
-        """The leveled circuit alone (fhe_score_batch): encrypt -> linear ->
-        decrypt, no key switch or bootstrap. T centres acc in the encoding.
-        Returns acc int64[B]."""
+    def score(self, q_x: torch.Tensor, w: torch.Tensor, cst: int, T: int, enc, id0: int = 0):
+        """The leveled circuit alone (fhe_score_batch[_key]): encrypt -> linear
+        -> decrypt, no key switch or bootstrap. T centres acc in the encoding;
+        `enc` as in compare(). Returns acc int64[B]."""
         B, D = q_x.shape
         acc = torch.empty(B, dtype=torch.int64, device=self.device)
-        self._chk(self._L.fhe_score_batch(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T),
-                                          C.c_uint64(enc_seed), C.c_uint64(id0), _ptr(acc), _stream(self.device)))
+        if isinstance(enc, (int, np.integer)):
+            rc = self._L.fhe_score_batch(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T), C.c_uint64(int(enc)),
+                                         C.c_uint64(id0), _ptr(acc), _stream(self.device))
+        else:
+            rc = self._L.fhe_score_batch_key(self._ctx, _ptr(q_x), B, D, _ptr(w), int(cst), int(T), self._key(enc),
+                                             C.c_uint64(id0), _ptr(acc), _stream(self.device))
+        self._chk(rc)
         return acc
 
     # ------------------------------------------- seeded (stored) corpus --
@@ -275,6 +300,10 @@ class Engine:
 
     @staticmethod
     def _key(k) -> C.Array:
+        if isinstance(k, (bytes, bytearray)):
+            if len(k) != 32:
+                raise ValueError("a ChaCha20 key is 32 bytes")
+            k = np.frombuffer(bytes(k), dtype="<u4")
         k = np.ascontiguousarray(k, dtype=np.uint32).reshape(8)
         return (C.c_uint32 * 8)(*[int(x) for x in k])
 

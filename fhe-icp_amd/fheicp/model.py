@@ -15,6 +15,7 @@ This is the engine behind the drop-in estimator (fheicp.sklearn). It owns
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -121,7 +122,7 @@ class FheLinearModel:
         self.engine = None
         self._w_dev = None
         self._enc_counter = 0
-        self.enc_seed = None
+        self.enc_seed = None     # session stream key (32 bytes), or an int seed in tests
 
     # ------------------------------------------------------------- fitting --
     @classmethod
@@ -134,16 +135,34 @@ class FheLinearModel:
         return cls(quantize_linear(X, coef, intercept, n_bits))
 
     # ------------------------------------------------------------- compile --
-    def compile(self, key_seed: int, device: int = 0, enc_seed: int | None = None, keys: dict | None = None):
-        """Create the device context and generate (or import) the keys."""
+    def compile(self, key_seed: int | None = None, device: int = 0, enc_seed: int | None = None,
+                keys: dict | None = None):
+        """Create the device context and generate (or import) the keys.
+
+        Keys: imported (``keys``), or generated from 32 bytes of os.urandom
+        through fhe_keygen_key; an explicit ``key_seed`` selects the 64-bit
+        seed form (fhe_keygen, reproducible tests and benches only).
+        Encryption: every compile starts a session with its own 256-bit stream
+        key from os.urandom, never derived from the key material, and a random
+        64-bit start for the stream ids, so two sessions (two processes with
+        the same configured key_seed included) never share masks or noise.
+        Nothing persisted lets the stream key be recomputed. ``enc_seed``
+        (tests only) replaces it with a seeded stream starting at id 0."""
         from .engine import Engine
         self.engine = Engine(self.scheme, device)
         if keys is not None:
             self.engine.import_keys(keys)
+        elif key_seed is not None:
+            self.engine.keygen(seed=int(key_seed))
         else:
-            self.engine.keygen(key_seed)
+            self.engine.keygen(key=os.urandom(32))
         self._w_dev = self.engine.to_dev(np.asarray(self.qparams.q_w, dtype=np.int64))
-        self.enc_seed = (key_seed ^ 0x5DEECE66D) if enc_seed is None else enc_seed
+        if enc_seed is None:
+            self.enc_seed = os.urandom(32)
+            self._enc_counter = int.from_bytes(os.urandom(8), "little")
+        else:
+            self.enc_seed = int(enc_seed)
+            self._enc_counter = 0
         return self
 
     @property
@@ -170,9 +189,20 @@ class FheLinearModel:
         return qx
 
     def next_id0(self, count: int) -> int:
+        """Stream ids [id0, id0 + count) of the next batch (mod 2^64: the
+        kernels add per-row offsets to a u64 id0)."""
         id0 = self._enc_counter
-        self._enc_counter += count
+        self._enc_counter = (self._enc_counter + count) & 0xFFFFFFFFFFFFFFFF
         return id0
+
+    def encrypt_linear(self, qx_dev, T: int = 0):
+        """The client encryption + leveled dot product alone, under this
+        session's stream key: big LWEs [B, kN + 1] of acc - T (device)."""
+        if self.engine is None:
+            raise RuntimeError("Model not compiled. Call compile() first.")
+        B, D = qx_dev.shape
+        return self.engine.encrypt_linear(qx_dev, self._w_dev, self.qparams.cst - int(T), self.enc_seed,
+                                          self.next_id0(B * D))
 
     def encrypted_acc(self, qx_dev, T: int = 0):
         """Run the fused encrypted compare on quantized inputs (device)."""

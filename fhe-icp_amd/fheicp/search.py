@@ -20,10 +20,16 @@ def sharded_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx
                  world: int = 1, group=None):
     """topk_fn(acc, below, k, base_idx) -> (acc_k, idx_k), missing slots idx -1.
 
-    Returns the global top-k (identical on every rank)."""
+    Returns the global top-k (identical on every rank). The exchange runs
+    whenever a process group exists, a one-rank group included (so a
+    one-GPU launcher run executes the RCCL all-gather too); without one,
+    world must be 1."""
     oa, oi = topk_fn(acc, below, k, base_idx)
-    if world == 1:
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        if world != 1:
+            raise RuntimeError(f"sharded_topk: world {world} without a process group")
         return oa, oi
+    world = torch.distributed.get_world_size(group)
     # one collective: the k (acc, index) pairs travel packed as [k, 2] int64.
     # RCCL gathers device tensors in place; other backends (gloo rehearsals)
     # go through host copies

@@ -107,10 +107,13 @@ size_t fhe_small_lwe_words(const fhe_params* params); /* n + 1 */
 /* ---- keys ----------------------------------------------------------------
  * Replaces Concrete keygen inside compile() (fhe_similarity.py:120) and the
  * key material FHEKeyManager.generate_keys means to persist
- * (key_management.py:112-191). Deterministic in `seed` (ChaCha20 streams,
- * DESIGN.md §3.1); fhe_keygen_key takes a full 256-bit ChaCha key. */
-int fhe_keygen(fhe_ctx* ctx, uint64_t seed, void* stream);
+ * (key_management.py:112-191). Every key word is a ChaCha20 stream word
+ *  under a 256-bit key. fhe_keygen_key is the production entry:
+ * pass 32 bytes from the OS CSPRNG. fhe_keygen expands a 64-bit seed by
+ * splitmix64 — 64 bits of entropy, NOT for production keys: reproducible
+ * tests, fixtures and benches only. */
 int fhe_keygen_key(fhe_ctx* ctx, const uint32_t h_key[8], void* stream);
+int fhe_keygen(fhe_ctx* ctx, uint64_t seed, void* stream);
 /* Host copies of the canonical key material; any pointer may be NULL.
  * s_small: n words (0/1); s_big: k*N words (0/1); bsk: fhe_bsk_words
  * (coefficient domain, [i][row][component][coef]); ksk: fhe_ksk_words
@@ -130,7 +133,15 @@ int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk);
 
 /* ---- client side: encrypt / decrypt --------------------------------------
  * Replaces the per-sample encrypt/decrypt of predict(fhe="execute")
- * (fhe_similarity.py:151). Ciphertext c uses stream id (id0 + c). */
+ * (fhe_similarity.py:151). Ciphertext c uses stream id (id0 + c).
+ * Encryption randomness. Every encrypting entry point comes in two forms:
+ * `*_key` takes the 256-bit ChaCha20 stream key (h_key / h_enc_key, 8 words),
+ * the production form — one fresh CSPRNG key per session, independent of the
+ * secret key's, with a random 64-bit id0 start, and stream ids (id0 + ...)
+ * never reused under one key; the plain form takes a 64-bit `seed`
+ * expanded by splitmix64 (fhe_key_from_seed): tests and benches only. */
+int fhe_encrypt_batch_key(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, const uint32_t h_key[8], uint64_t id0,
+                          uint64_t* d_ct, void* stream);
 int fhe_encrypt_batch(fhe_ctx* ctx, const int64_t* d_msg, int64_t count, uint64_t seed, uint64_t id0,
                       uint64_t* d_ct, void* stream);
 /* round(phase / Delta) as signed msg_bits-bit integers */
@@ -151,6 +162,8 @@ int fhe_linear_batch(fhe_ctx* ctx, const uint64_t* d_ct, int64_t B, int32_t D, c
  * of row b (d_qx, B x D, encoded at Delta) are the first coefficients of
  * G = ceil(D / N) GLWE messages; GLWE (b, g) uses stream id id0 + b*G + g.
  * d_glwe: B x G x (k+1)N words [A_1 .. A_k, B] per GLWE. */
+int fhe_encrypt_packed_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const uint32_t h_key[8],
+                                 uint64_t id0, uint64_t* d_glwe, void* stream);
 int fhe_encrypt_packed_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
                              uint64_t* d_glwe, void* stream);
 /* The leveled dot product on packed inputs (Concrete-ML
@@ -163,6 +176,8 @@ int fhe_linear_packed_batch(fhe_ctx* ctx, const uint64_t* d_glwe, int64_t B, int
  * GLWEs are never written (bit-identical to the two calls). The single-party
  * form of predict(fhe="execute"): client encryption and the server's leveled
  * dot product in one pass; d_out: B x (kN+1). */
+int fhe_encrypt_linear_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const uint32_t h_key[8],
+                                 uint64_t id0, const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream);
 int fhe_encrypt_linear_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, uint64_t seed, uint64_t id0,
                              const int64_t* d_w, int64_t cst, uint64_t* d_out, void* stream);
 /* big -> small key switch of (ct << shift) + add_body (shift/add used by the
@@ -249,7 +264,12 @@ int fhe_threshold_batch(fhe_ctx* ctx, const uint64_t* d_ct_acc, int64_t count, i
  *   bootstrapped threshold bit; acc >= T <=> score >= min_similarity).
  * Uses context-owned workspace of ~8 * B * (2(kN+1) + n + 2) bytes (grown on
  * demand; not graph-capturable): the encryption is fused into the linear step
- * (fhe_encrypt_linear_batch), so D does not enter the footprint. */
+ * (fhe_encrypt_linear_batch), so D does not enter the footprint. The `_key`
+ * form takes the session's 256-bit encryption key (see "Encryption
+ * randomness"); the enc_seed form is for tests and benches. */
+int fhe_compare_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                          int64_t T, const uint32_t h_enc_key[8], uint64_t id0, int64_t* d_acc, int64_t* d_below,
+                          void* stream);
 int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                       int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, int64_t* d_below, void* stream);
 /* The reference's predict(fhe="execute") as it is (fhe_similarity.py:142-160,
@@ -257,7 +277,10 @@ int fhe_compare_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, c
  * -> linear with d_w and cst - T -> decrypt; d_acc[b] = the accumulator
  * (exact int64). No key switch or bootstrap runs; T only centres the value in
  * the msg_bits-bit encoding (acc - T must fit it; the estimator passes the
- * middle of the accumulator range). Workspace ~8 * B * (kN + 2) bytes. */
+ * middle of the accumulator range). Workspace ~8 * B * (kN + 2) bytes.
+ * `_key` form: the session's 256-bit encryption key, as fhe_compare_batch_key. */
+int fhe_score_batch_key(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
+                        int64_t T, const uint32_t h_enc_key[8], uint64_t id0, int64_t* d_acc, void* stream);
 int fhe_score_batch(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int32_t D, const int64_t* d_w, int64_t cst,
                     int64_t T, uint64_t enc_seed, uint64_t id0, int64_t* d_acc, void* stream);
 
@@ -289,8 +312,9 @@ int fhe_linear_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t
 int fhe_compare_seeded_batch(fhe_ctx* ctx, const uint64_t* d_body, const uint64_t* d_id0, int64_t B, int32_t D,
                              const uint32_t h_mask_key[8], const int64_t* d_w, int64_t cst, int64_t T,
                              int64_t* d_acc, int64_t* d_below, void* stream);
-/* The 64-bit-seed -> 256-bit ChaCha key expansion used by fhe_keygen and
- * fhe_encrypt_batch (splitmix64). Host only. */
+/* The 64-bit-seed -> 256-bit ChaCha key expansion used by the seed forms
+ * (fhe_keygen, fhe_encrypt_batch, ...; splitmix64): tests and
+ * benches only. Host only. */
 void fhe_key_from_seed(uint64_t seed, uint32_t h_key_out[8]);
 
 /* ---- clear pre/post-processing on the device ----------------------------

@@ -6,8 +6,13 @@ fhe_similarity.py to call the MI355X engine through its C ABI
 kept here, runnable, so tests/test_gpu_dropin.py can prove that the binding
 works as written.
 
-    eng = GpuCompare(params_dict, key_seed=1234, lib_path=".../libfheicp.so")
+    eng = GpuCompare(params_dict, lib_path=".../libfheicp.so")
     acc, below = eng.compare(q_x, q_w, cst, T)   # int64 numpy arrays
+
+Keys come from 32 bytes of os.urandom (fhe_keygen_key) and every session
+encrypts under its own 32-byte stream key with a random 64-bit id start
+(fhe_compare_batch_key / fhe_score_batch_key). key_seed / enc_seed select the
+64-bit seed forms, for reproducible tests only.
 """
 from __future__ import annotations
 
@@ -33,6 +38,7 @@ _PROTOS = {
     "fhe_ctx_destroy": (None, [_vp]),
     "fhe_last_error": (C.c_char_p, [_vp]),
     "fhe_keygen": (C.c_int, [_vp, _u64, _vp]),
+    "fhe_keygen_key": (C.c_int, [_vp, _vp, _vp]),
     "fhe_dev_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
     "fhe_dev_free": (C.c_int, [_vp, _vp]),
     "fhe_memcpy_h2d": (C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp]),
@@ -40,13 +46,20 @@ _PROTOS = {
     "fhe_compare_batch": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     "fhe_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp]),
     "fhe_score_batch": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp]),
+    "fhe_compare_batch_key": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _u64, _vp, _vp, _vp]),
+    "fhe_score_batch_key": (C.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _u64, _vp, _vp]),
 }
+
+
+def _key32() -> C.Array:
+    """A 256-bit ChaCha20 key (8 u32 words) from the OS CSPRNG."""
+    return (C.c_uint32 * 8).from_buffer_copy(os.urandom(32))
 
 
 class GpuCompare:
     """One device context + keys; batched encrypted compares from numpy."""
 
-    def __init__(self, params: dict, key_seed: int, device: int = 0, lib_path: str | None = None,
+    def __init__(self, params: dict, key_seed: int | None = None, device: int = 0, lib_path: str | None = None,
                  enc_seed: int | None = None):
         path = lib_path or os.environ.get("FHEICP_LIB", "libfheicp.so")
         self.L = L = C.CDLL(path)
@@ -56,9 +69,20 @@ class GpuCompare:
         self.P = fhe_params(**{f: int(params.get(f, 0)) for f in FIELDS})
         self.ctx = _vp()
         self._ok(L.fhe_ctx_create(C.byref(self.P), device, C.byref(self.ctx)))
-        self._ok(L.fhe_keygen(self.ctx, key_seed, None))
-        self.enc_seed = enc_seed if enc_seed is not None else key_seed ^ 0x5DEECE66D
-        self.next_id = 0
+        if key_seed is None:
+            self._ok(L.fhe_keygen_key(self.ctx, _key32(), None))
+        else:
+            self._ok(L.fhe_keygen(self.ctx, key_seed, None))  # 64-bit seed: tests only
+        # the session's encryption stream: its own 256-bit key and a random id
+        # start (enc_seed: the seeded test form, ids from 0)
+        self.enc_seed = enc_seed
+        self.enc_key = None if enc_seed is not None else _key32()
+        self.next_id = 0 if enc_seed is not None else int.from_bytes(os.urandom(8), "little")
+
+    def _take_ids(self, count: int) -> int:
+        id0 = self.next_id
+        self.next_id = (self.next_id + count) & 0xFFFFFFFFFFFFFFFF
+        return id0
 
     def _ok(self, rc: int) -> None:
         if rc != 0:
@@ -88,9 +112,14 @@ class GpuCompare:
         B, D = q_x.shape
         bufs = [self._to_dev(q_x), self._to_dev(np.asarray(q_w, np.int64)), self._alloc(8 * B), self._alloc(8 * B)]
         try:
-            self._ok(self.L.fhe_compare_batch(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(T), self.enc_seed,
-                                              self.next_id, bufs[2], bufs[3], None))
-            self.next_id += B * D
+            id0 = self._take_ids(B * D)
+            if self.enc_key is not None:
+                rc = self.L.fhe_compare_batch_key(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(T), self.enc_key,
+                                                  id0, bufs[2], bufs[3], None)
+            else:
+                rc = self.L.fhe_compare_batch(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(T), self.enc_seed,
+                                              id0, bufs[2], bufs[3], None)
+            self._ok(rc)
             return self._to_host(bufs[2], B), self._to_host(bufs[3], B)
         finally:
             for d in bufs:
@@ -106,9 +135,14 @@ class GpuCompare:
         B, D = q_x.shape
         bufs = [self._to_dev(q_x), self._to_dev(np.asarray(q_w, np.int64)), self._alloc(8 * B)]
         try:
-            self._ok(self.L.fhe_score_batch(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(centre), self.enc_seed,
-                                            self.next_id, bufs[2], None))
-            self.next_id += B * D
+            id0 = self._take_ids(B * D)
+            if self.enc_key is not None:
+                rc = self.L.fhe_score_batch_key(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(centre), self.enc_key,
+                                                id0, bufs[2], None)
+            else:
+                rc = self.L.fhe_score_batch(self.ctx, bufs[0], B, D, bufs[1], int(cst), int(centre), self.enc_seed,
+                                            id0, bufs[2], None)
+            self._ok(rc)
             return self._to_host(bufs[2], B)
         finally:
             for d in bufs:

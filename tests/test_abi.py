@@ -110,7 +110,9 @@ def test_build_info_and_kernel_names_on_host_context():
     kernels (empty names), rejects unknown buckets, and the table bootstrap
     and threshold entries refuse without a device."""
     L = _lib.lib()
-    assert L.fhe_build_info() == b"libfheicp gfx950 ab=0"
+    import __graft_entry__ as G
+    # the library in the tree was compiled from these very sources
+    assert L.fhe_build_info() == b"libfheicp gfx950 ab=0 src=" + G.source_sha().encode()
     assert not _lib.ab_build()
     P = _lib.params_struct(params_for_bits(16).as_dict())
     h = C.c_void_p()

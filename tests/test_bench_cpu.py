@@ -99,3 +99,46 @@ def test_leveled_mix_floor():
     f1 = bench.leveled_mix_floor_s(p, 16, 1)
     assert abs(bench.leveled_mix_floor_s(p, 16, 1024) - 1024 * f1) < 1e-15
     assert f1 > bench.leveled_ops_per_pair(p, 16) / (bench.VALU_PEAK_TOPS * 1e12)
+
+
+def test_one_rank_launcher_creates_the_group(tmp_path):
+    """WORLD_SIZE=1 under a launcher: dist_setup joins a process group (gloo
+    here, RCCL on the GPU box) and sharded_topk runs its all-gather, so a
+    one-GPU launcher run exercises the N-rank code path."""
+    code = r"""
+import os, sys, torch
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import bench
+from fheicp.search import sharded_topk, host_topk
+class A: pass
+world, rank, local = bench.dist_setup(A())
+assert (world, rank) == (1, 0) and bench.dist_on()
+assert torch.distributed.get_backend() == "gloo"
+calls = []
+orig = torch.distributed.all_gather
+torch.distributed.all_gather = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+oa, oi = sharded_topk(torch.tensor([3, 8, 8, 1]), None, 2, 10, host_topk, 1)
+assert calls == [1] and oa.tolist() == [8, 8] and oi.tolist() == [11, 12], (calls, oa, oi)
+torch.distributed.destroy_process_group()
+open(os.path.join(sys.argv[3], "ok"), "w").close()
+"""
+    script = tmp_path / "one.py"
+    script.write_text(code)
+    env = dict(os.environ, FHEICP_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(script),
+           str(REPO / "fhe-icp_amd"), str(REPO), str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (tmp_path / "ok").exists()
+
+
+def test_bare_single_rank_has_no_group():
+    """Run bare at N = 1 (the driver's default line) no group exists and
+    sharded_topk is the local top-k alone."""
+    sys.path.insert(0, str(REPO))
+    import torch
+    from fheicp.search import sharded_topk, host_topk
+    assert not torch.distributed.is_initialized()
+    oa, oi = sharded_topk(torch.tensor([1, 5]), None, 1, 0, host_topk, 1)
+    assert oa.tolist() == [5] and oi.tolist() == [1]

@@ -32,6 +32,18 @@ def toy(need_gpu, oracle_lib):
 
 
 @pytest.fixture(scope="module")
+def toy_k1(need_gpu, oracle_lib):
+    """k = 1, N = 256: kN = 256 mask words, so k_encrypt_linear's wave 0 owns
+    words only on lanes 0-31 (the weights' v_readlane broadcast still reads
+    lanes 32-63: ADVICE r04)."""
+    P = replace(TOY, k=1)
+    eng = Engine(P, 0)
+    eng.keygen(4321)
+    ref = oracle_lib.RefTFHE(P.as_dict(), 4321)
+    return eng, ref
+
+
+@pytest.fixture(scope="module")
 def real(need_gpu, oracle_lib):
     eng = Engine(REAL16, 0)
     eng.keygen(777)
@@ -488,7 +500,7 @@ def test_threshold_batch_real(real):
     assert np.array_equal(ref.decrypt_bits(b_ref), (acc[:4] >= T).astype(np.int64))
 
 
-@pytest.mark.parametrize("which", ["toy", "real"])
+@pytest.mark.parametrize("which", ["toy", "real", "toy_k1"])
 def test_encrypt_linear_fused_bit_exact(which, request):
     """fhe_encrypt_linear_batch (the fused client encryption + leveled dot of
     fhe_compare_batch / fhe_score_batch, packed features: DESIGN.md §3.2) is

@@ -154,3 +154,30 @@ def test_bench_gpus2_without_launcher(need_gpu):
     assert par["ranks"] == 2 and par["compares_checked"] == 4096
     assert par["acc_bit_exact"] and par["threshold_bit_exact"] and par["quant_params_equal"]
     assert out["topk_check"]["indices_equal"] and out["topk_check"]["scores_equal"]
+
+
+def test_bench_one_rank_rccl(need_gpu):
+    """The RCCL path on the one GPU of this box: bench.py under
+    torch.distributed.run with one rank and the default backend ("nccl" =
+    RCCL), so the process group, the barriers, the MAX/MIN/SUM all-reduces of
+    the timing and parity flags and the top-k all-gather all execute on the
+    device through RCCL (the 8-GPU run's code path, at world size 1)."""
+    env = {k: v for k, v in os.environ.items() if k != "FHEICP_DIST_BACKEND"}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"),
+           "--gpus", "1", "--workload", "c4", "--total-docs", "4096", "--steps", "1", "--warmup", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=str(REPO), env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["config"]["total_docs"] == 4096
+    assert out["dist"]["backend"] == "nccl" and out["dist"]["rccl"] and out["dist"]["device"].startswith("cuda")
+    par = out["parity"]
+    assert par["ranks"] == 1 and par["compares_checked"] == 4096
+    assert par["acc_bit_exact"] and par["threshold_bit_exact"] and par["quant_params_equal"]
+    assert out["topk_check"]["indices_equal"] and out["topk_check"]["scores_equal"]
+    assert out["allgather_ms"] > 0
+    assert "RCCL top-k all-gather" in out["config"]["workload"]
