@@ -66,8 +66,15 @@ __host__ __device__ constexpr int jof(int li, int lane, int u) {
 // LA <-> LB is not an LDS relayout any more: it exchanges the slot bits with
 // lane bits 3..5 in registers (swap_lb below); only LB <-> LC goes through
 // LDS (offsets from tools/search_relayout.py --lb 0,1,2,6,7,8).
-enum { R2F = 0, R2I = 1 };  // LB->LC, LC->LB
-constexpr int RC[2][5] = {{1, 2, 4, 7, 16}, {2, 4, 8, 16, 31}};
+// FHEICP_ABLDS = 1: LA <-> LB through the slot too (R1F / R1I, offsets from
+// tools/search_relayout.py; the identity is conflict-free for LB -> LA)
+// instead of the permlane / DPP swaps (8.3 and 4.2 SIMD cycles per
+// instruction, tools/xlane_probe.hip: 32 + 32 per transform)
+#ifndef FHEICP_ABLDS
+#define FHEICP_ABLDS 0
+#endif
+enum { R2F = 0, R2I = 1, R1F = 2, R1I = 3 };  // LB->LC, LC->LB, LA->LB, LB->LA
+constexpr int RC[4][5] = {{1, 2, 4, 7, 16}, {2, 4, 8, 16, 31}, {2, 4, 8, 16, 30}, {0, 0, 0, 0, 0}};
 __host__ __device__ constexpr int rpos(int r, int j) {
   int p = j;
   for (int k = 0; k < 5; ++k) p += RC[r][k] * ((j >> (4 + k)) & 1);
@@ -305,7 +312,6 @@ __device__ __forceinline__ void swap_lb(c64 (&v)[S]) {
   swap_bit<1, 2>(v);
   swap_bit<2, 1>(v);
 }
-
 // folded coefficient pairs (a_t + i a_{t+M}), natural order (LA) -> LC;
 // includes the negacyclic twist w^t
 template <int DBG = 0, int NR = 0>
@@ -314,7 +320,8 @@ __device__ __forceinline__ void forward(c64 (&v)[S], const c64* twl, c64* scr, i
   fold8<false>(v);
   dft8(v);
   lane_tw<0, false, DBG, NR>(v, twl, lane, wf, treg);
-  if constexpr ((DBG & 8) == 0) swap_lb(v);
+  if constexpr (FHEICP_ABLDS) relayout<R1F, LA, LB, DBG>(v, scr, lane);
+  else if constexpr ((DBG & 8) == 0) swap_lb(v);
   dft8(v);
   lane_tw<1, false, DBG>(v, twl, lane, wf);
   relayout<R2F, LB, LC, DBG>(v, scr, lane);
@@ -328,7 +335,8 @@ __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, i
   relayout<R2I, LC, LB, DBG>(v, scr, lane);
   lane_tw<1, true, DBG>(v, twl, lane, wf);
   idft8(v);
-  if constexpr ((DBG & 8) == 0) swap_lb(v);
+  if constexpr (FHEICP_ABLDS) relayout<R1I, LB, LA, DBG>(v, scr, lane);
+  else if constexpr ((DBG & 8) == 0) swap_lb(v);
   lane_tw<0, true, DBG, NR>(v, twl, lane, wf, treg);
   idft8(v);
   fold8<true>(v);
@@ -337,11 +345,12 @@ __device__ __forceinline__ void inverse(c64 (&v)[S], const c64* twl, c64* scr, i
 // the inverse from layout LB on (after the C -> B relayout's writes and reads,
 // which a caller may have split between waves)
 template <int DBG = 0, int NR = 0>
-__device__ __forceinline__ void inverse_post(c64 (&v)[S], const c64* twl, int lane, c64 wf = {},
+__device__ __forceinline__ void inverse_post(c64 (&v)[S], const c64* twl, c64* scr, int lane, c64 wf = {},
                                              const c64* treg = nullptr) {
   lane_tw<1, true, DBG>(v, twl, lane, wf);
   idft8(v);
-  if constexpr ((DBG & 8) == 0) swap_lb(v);
+  if constexpr (FHEICP_ABLDS) relayout<R1I, LB, LA, DBG>(v, scr, lane);
+  else if constexpr ((DBG & 8) == 0) swap_lb(v);
   lane_tw<0, true, DBG, NR>(v, twl, lane, wf, treg);
   idft8(v);
   fold8<true>(v);

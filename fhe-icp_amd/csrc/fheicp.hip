@@ -1141,6 +1141,11 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
     if (ctx->mb_dbg) {
       const int w = ctx->mb_dbg >> 8;
       if (ctx->mb_dbg == 2) { if (p.pbs_level == 1) MBD(1, 2, 0); else MBD(2, 2, 0); }
+      else if (ctx->mb_dbg == 16) { if (p.pbs_level == 1) MBD(1, 16, 0); else MBD(2, 16, 0); }
+      else if (ctx->mb_dbg == 32) { if (p.pbs_level == 1) MBD(1, 32, 0); else MBD(2, 32, 0); }
+      else if (ctx->mb_dbg == 48) { if (p.pbs_level == 1) MBD(1, 48, 0); else MBD(2, 48, 0); }
+      else if (ctx->mb_dbg == 64) { if (p.pbs_level == 1) MBD(1, 64, 0); else MBD(2, 64, 0); }
+      else if (ctx->mb_dbg == 18) { if (p.pbs_level == 1) MBD(1, 18, 0); else MBD(2, 18, 0); }
       else if (ctx->mb_dbg == 130) { if (p.pbs_level == 1) MBD(1, 130, 0); else MBD(2, 130, 0); }
       else if (w == 0) { if (p.pbs_level == 1) MBD(1, 128, 0); else MBD(2, 128, 0); }
       else if (w == 1) { if (p.pbs_level == 1) MBD(1, 128 + 256, 0); else MBD(2, 128 + 256, 0); }
@@ -1487,7 +1492,11 @@ static int sign_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uin
   if (count < PIPE_MIN || off) return sign_extract(ctx, d_ct_v, count, d_sign, small, st, 0);
   const fhe_params& p = ctx->p;
   const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
-  const int64_t c0 = ((count / 2) + 3) & ~(int64_t)3, c1 = count - c0;  // whole workgroups of 4
+  // the first half a whole number of 1024-ciphertext waves (256 four-ciphertext
+  // workgroups, one per CU) nearest count / 2, so only the second half ends on
+  // a partial wave: at 12,500 (a C4 shard) 6144 + 6356 runs 13 rounds of
+  // workgroups where 6252 + 6248 ran 14 (6.1 waves each)
+  const int64_t c0 = std::min(std::max((int64_t)1024, 1024 * ((count + 1024) / 2048)), count - 4), c1 = count - c0;
   for (int l = 0; l < 2; ++l)
     if (!ctx->lane_st[l]) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->lane_st[l], hipStreamNonBlocking));
   for (int l = 0; l < 3; ++l)

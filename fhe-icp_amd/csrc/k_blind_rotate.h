@@ -727,8 +727,9 @@ __host__ __device__ constexpr int psi_pos(int x) { return x ^ ((x >> 4) & 15); }
 //   per pair: digits -> [forward -> F to slot -> barrier -> products for the
 //   quarter -> barrier] x L -> products to the owners' slots -> barrier ->
 //   own slot -> inverse
-// DBG != 0 only in A/B timing builds: 2 = no key loads (wrong results), 128 =
-// phase timestamps of wave DBG >> 8 of workgroup 0, pairs 100..103.
+// DBG != 0 only in A/B timing builds (wrong results): 2 = no key loads, 16 = no
+// psi gathers, 32 = no F reads, 64 = no F stores; 128 = phase timestamps of
+// wave DBG >> 8 of workgroup 0, pairs 100..103 (results correct).
 // BETA != 0: the gadget base log as a constant (the shipped fast gadgets),
 // which folds the digit shifts and widths into inline operands; 0 = `beta`.
 // Key rows come through buffer loads: a per-lane offset fixed for the kernel
@@ -933,8 +934,10 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
       // 4.06 vs 4.04 ms per 1024, not kept)
       forward<0, NR>(v, twl, slot, lane, {}, treg);
       V4_STAMP(2 + 4 * lv);
+      if constexpr ((DBG & 64) == 0) {
 #pragma unroll
-      for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
+        for (int u = 0; u < S; ++u) slot[u * 64 + lane] = v[u];
+      }
       load(0, kb[0]);
       V4_STAMP(3 + 4 * lv);
       lds_barrier();
@@ -958,7 +961,9 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
         for (int gg = 0; gg < G; ++gg) {
           c64 F[WPC];
 #pragma unroll
-          for (int r = 0; r < WPC; ++r) F[r] = xbuf[(gg * WPC + r) * SCR + (XP ? fpos + t * 64 : u * 64 + lane)];
+          for (int r = 0; r < WPC; ++r)
+            F[r] = (DBG & 32) ? c64{v[(gg + r) & 7].x, v[(gg + 2 * r + t) & 7].y}
+                              : xbuf[(gg * WPC + r) * SCR + (XP ? fpos + t * 64 : u * 64 + lane)];
 #pragma unroll
           for (int Ss = 0; Ss < 3; ++Ss) {
             c64 P = {0.0, 0.0};
@@ -972,7 +977,10 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
               pa[gg][Ss] ^= (aS[gg][Ss] & 1u) << 14;
             }
             // the table holds psi^x - 1
-            cmac(o[gg][t], *reinterpret_cast<const c64*>(reinterpret_cast<const char*>(psil) + pa[gg][Ss]), P);
+            if constexpr ((DBG & 16) != 0)
+              cmac(o[gg][t], c64{__builtin_bit_cast(double, (u64)pa[gg][Ss] | 0x3fe0000000000000ull), 0.25}, P);
+            else
+              cmac(o[gg][t], *reinterpret_cast<const c64*>(reinterpret_cast<const char*>(psil) + pa[gg][Ss]), P);
           }
         }
       }
@@ -1001,7 +1009,7 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
       V4_STAMP(10);
 #pragma unroll
       for (int u = 0; u < S; ++u) ov[u] = slot[rpos(R2I, jof(LB, lane, u))];
-      inverse_post<0, NR>(ov, twl, lane, {}, treg);
+      inverse_post<0, NR>(ov, twl, slot, lane, {}, treg);
     } else {
       // products to the owners: ciphertext gg's component comp, slots 2g, 2g+1
 #pragma unroll

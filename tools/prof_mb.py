@@ -21,7 +21,11 @@ ap.add_argument("--P", type=int, default=21)
 ap.add_argument("--lib", default="")
 ap.add_argument("--tag", default="")
 ap.add_argument("--stamps", type=int, default=-1, help="A/B build: phase timestamps of this wave (FHEICP_MB_DBG); 99: wave 0 without BSK loads")
+ap.add_argument("--dbg", type=int, default=0, help="A/B build: FHEICP_MB_DBG timing variant (2 no key loads, 16 no psi "
+                "gathers, 32 no F reads, 48 both, 64 no F stores, 18 no loads + no psi; wrong results)")
 a = ap.parse_args()
+if a.dbg:
+    os.environ["FHEICP_MB_DBG"] = str(a.dbg)
 if a.stamps >= 0:
     os.environ["FHEICP_MB_DBG"] = str(130 if a.stamps == 99 else 128 + 256 * a.stamps)
 if a.lib:
