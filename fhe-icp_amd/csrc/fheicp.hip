@@ -1489,14 +1489,20 @@ static int sign_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uin
     const char* e = getenv("FHEICP_PIPE");
     return e && atoi(e) == 0;
   }();
-  if (count < PIPE_MIN || off) return sign_extract(ctx, d_ct_v, count, d_sign, small, st, 0);
+  static const int64_t pipe_min = [] {  // FHEICP_PIPE_MIN: A/B runs of the threshold
+    const char* e = getenv("FHEICP_PIPE_MIN");
+    return e ? (int64_t)std::max(8, atoi(e)) : PIPE_MIN;
+  }();
+  if (count < pipe_min || off) return sign_extract(ctx, d_ct_v, count, d_sign, small, st, 0);
   const fhe_params& p = ctx->p;
   const size_t Wb = fhe_big_lwe_words(&p), Ws = fhe_small_lwe_words(&p);
   // the first half a whole number of 1024-ciphertext waves (256 four-ciphertext
   // workgroups, one per CU) nearest count / 2, so only the second half ends on
   // a partial wave: at 12,500 (a C4 shard) 6144 + 6356 runs 13 rounds of
   // workgroups where 6252 + 6248 ran 14 (6.1 waves each)
-  const int64_t c0 = std::min(std::max((int64_t)1024, 1024 * ((count + 1024) / 2048)), count - 4), c1 = count - c0;
+  const int64_t c0 = count < 2048 ? ((count / 2) + 3) & ~(int64_t)3
+                                  : std::min(std::max((int64_t)1024, 1024 * ((count + 1024) / 2048)), count - 4),
+                c1 = count - c0;
   for (int l = 0; l < 2; ++l)
     if (!ctx->lane_st[l]) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->lane_st[l], hipStreamNonBlocking));
   for (int l = 0; l < 3; ++l)
