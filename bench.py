@@ -229,7 +229,7 @@ def read_br(eng) -> dict:
     """Blind-rotation HIP-event totals per gadget (fhe_profile_read) and the
     instantiation each launched (fhe_profile_kernel_name)."""
     out = {}
-    for g in ("main", "mid", "mid2", "fast", "fast2"):
+    for g in ("main", "mid0", "mid", "mid2", "fast", "fast2"):
         out[g] = eng.profile_read(f"blind_rotate_{g}")
         out[g]["kernel"] = eng.kernel_name(f"blind_rotate_{g}")
     return out
@@ -279,7 +279,7 @@ def pipelined(batch: int) -> bool:
     return batch >= PIPE_MIN and os.environ.get("FHEICP_PIPE", "1") != "0"
 
 
-GADGET_ID = {"main": 0, "fast": 1, "fast2": 2, "mid": 3, "mid2": 4}
+GADGET_ID = {"main": 0, "fast": 1, "fast2": 2, "mid": 3, "mid2": 4, "mid0": 5}
 
 
 def isolated_br(eng, brs, reps: int = 3) -> dict:
@@ -319,12 +319,12 @@ def roofline(p, brs, batch: int = 0, iso: dict | None = None) -> dict:
     FMA x2) / the HIP-event launch time on the kernel's stream. The HBM view
     (algorithmic bytes / time against 8 TB/s, and the PMC-measured bytes as
     `traffic`) stays beside it. With per-round gadgets up to
-    five gadgets run; the kernel with the largest total time is reported, all
+    six gadgets run; the kernel with the largest total time is reported, all
     are listed under `kernels`."""
     from dataclasses import replace
     from fheicp.params import gadget_level, gadget_of
     qs = {}
-    for g, gid in (("main", 0), ("mid", 3), ("mid2", 4), ("fast", 1), ("fast2", 2)):
+    for g, gid in (("main", 0), ("mid0", 5), ("mid", 3), ("mid2", 4), ("fast", 1), ("fast2", 2)):
         if gid == 0 or gadget_level(p, gid):
             bl, lv, grp = gadget_of(p, gid)
             qs[g] = (replace(p, pbs_base_log=bl, pbs_level=lv), grp)

@@ -48,10 +48,10 @@ struct fhe_ctx {
   u64 *s_small = nullptr, *s_big = nullptr, *bsk = nullptr, *ksk = nullptr, *ksk_colsum = nullptr;
   c64 *bsk_fft = nullptr, *tw = nullptr, *twist = nullptr, *tw4 = nullptr;
   c64* bsk_fft_v2 = nullptr;  // v2-layout copy of the main BSK for the table bootstrap (made on first use)
-  // bootstrapping keys of the other gadgets (g = 1..4: p.pbs_fast_*,
-  // pbs_fast2_*, pbs_mid_*, pbs_mid2_*), coefficient domain and FFT form
-  u64* bskf[4] = {nullptr, nullptr, nullptr, nullptr};
-  c64* bskf_fft[4] = {nullptr, nullptr, nullptr, nullptr};
+  // bootstrapping keys of the other gadgets (g = 1..5: p.pbs_fast_*,
+  // pbs_fast2_*, pbs_mid_*, pbs_mid2_*, pbs_mid0_*), coefficient domain and FFT form
+  u64* bskf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  c64* bskf_fft[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   // multi-bit blind rotation of the fast gadgets with pbs_fast*_group = 2
   // (DESIGN.md §4.5): their keys hold three GGSWs per pair of LWE
   // coefficients (messages in mb_msg); psi^x table, x < 2N (bank-swizzled)
@@ -63,7 +63,7 @@ struct fhe_ctx {
   void* ws = nullptr;
   size_t ws_bytes = 0;
   bool prof = false;
-  ProfAcc prof_br, prof_brf[4], prof_ks;  // blind rotation on the main / fast / fast2 / mid / mid2 gadget
+  ProfAcc prof_br, prof_brf[5], prof_ks;  // blind rotation on the main / fast / fast2 / mid / mid2 / mid0 gadget
   ProfAcc prof_enc;                       // the fused client encryption + leveled dot (k_encrypt_linear)
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2
                        // (two waves per ciphertext; forced by FHEICP_BR_VARIANT=2), 3 (A/B builds)
@@ -152,14 +152,22 @@ static int validate(const fhe_params* p, std::string& why) {
       (p->pbs_mid2_level && !p->pbs_mid_level)) {
     why = "mid2 pbs decomposition out of range (0, 0 for none; needs the mid gadget)"; return -1;
   }
-  for (int g = 1; g <= 4; ++g) {
+  if ((p->pbs_mid0_base_log == 0) != (p->pbs_mid0_level == 0) || p->pbs_mid0_level < 0 ||
+      p->pbs_mid0_level > 8 || p->pbs_mid0_base_log < 0 || p->pbs_mid0_level * p->pbs_mid0_base_log > 62 ||
+      (p->pbs_mid0_level && !p->pbs_mid_level)) {
+    why = "mid0 pbs decomposition out of range (0, 0 for none; needs the mid gadget)"; return -1;
+  }
+  for (int g = 1; g <= 5; ++g) {
     const int grp = g == 1 ? p->pbs_fast_group : g == 2 ? p->pbs_fast2_group : g == 3 ? p->pbs_mid_group
-                                                                                     : p->pbs_mid2_group;
+                    : g == 4 ? p->pbs_mid2_group : p->pbs_mid0_group;
     const int L = g == 1 ? p->pbs_fast_level : g == 2 ? p->pbs_fast2_level : g == 3 ? p->pbs_mid_level
-                                                                                    : p->pbs_mid2_level;
+                  : g == 4 ? p->pbs_mid2_level : p->pbs_mid0_level;
     const int bl = g == 1 ? p->pbs_fast_base_log : g == 2 ? p->pbs_fast2_base_log
-                                                          : g == 3 ? p->pbs_mid_base_log : p->pbs_mid2_base_log;
-    if (grp < 0 || grp > 2) { why = "pbs_fast_group / pbs_fast2_group / pbs_mid_group / pbs_mid2_group must be 0, 1 or 2"; return -1; }
+                   : g == 3 ? p->pbs_mid_base_log : g == 4 ? p->pbs_mid2_base_log : p->pbs_mid0_base_log;
+    if (grp < 0 || grp > 2) {
+      why = "pbs_fast_group / pbs_fast2_group / pbs_mid_group / pbs_mid2_group / pbs_mid0_group must be 0, 1 or 2";
+      return -1;
+    }
     // 32-bit accumulators when level <= 2 and level * base_log <= 31, else
     // 48-bit (k_blind_rotate_mb64), whose digits are read as 32-bit fields:
     // base_log <= 31 (a wider digit's f64 products are noise anyway)
@@ -178,8 +186,8 @@ static int validate(const fhe_params* p, std::string& why) {
 }
 
 // The bootstrap gadgets of a parameter set: 0 main (pbs_base_log,
-// pbs_level), 1 fast, 2 fast2, 3 mid, 4 mid2 (0 levels: absent).
-constexpr int NGAD = 5;
+// pbs_level), 1 fast, 2 fast2, 3 mid, 4 mid2, 5 mid0 (0 levels: absent).
+constexpr int NGAD = 6;
 static int gadget_level(const fhe_params& p, int g) {
   switch (g) {
     case 0: return p.pbs_level;
@@ -187,6 +195,7 @@ static int gadget_level(const fhe_params& p, int g) {
     case 2: return p.pbs_fast2_level;
     case 3: return p.pbs_mid_level;
     case 4: return p.pbs_mid2_level;
+    case 5: return p.pbs_mid0_level;
   }
   return 0;
 }
@@ -197,13 +206,14 @@ static int gadget_base_log(const fhe_params& p, int g) {
     case 2: return p.pbs_fast2_base_log;
     case 3: return p.pbs_mid_base_log;
     case 4: return p.pbs_mid2_base_log;
+    case 5: return p.pbs_mid0_base_log;
   }
   return 0;
 }
 // grouping factor of gadget g's blind rotation (the main gadget is classic)
 static int gadget_group(const fhe_params& p, int g) {
   const int v = g == 1 ? p.pbs_fast_group : g == 2 ? p.pbs_fast2_group : g == 3 ? p.pbs_mid_group
-                                                                               : g == 4 ? p.pbs_mid2_group : 1;
+                : g == 4 ? p.pbs_mid2_group : g == 5 ? p.pbs_mid0_group : 1;
   return v == 2 ? 2 : 1;
 }
 
@@ -289,7 +299,7 @@ static double plan_worst(const fhe_params& p, int d, const int* sched) {
 // bootstrap (sched[0..R), returns R). Without a fast gadget: the
 // single-gadget rule (d = 4 if its worst round keeps 9.2 sigma, else 3), all
 // rounds on the main gadget. With fast gadgets: the widest d (or the forced
-// one); then along the ladder main, mid, mid2, fast, fast2 (those present,
+// one); then along the ladder main, mid0, mid, mid2, fast, fast2 (those present,
 // noisier down the ladder) each gadget takes the fewest leading rounds for
 // which the next gadget on all the remaining ones keeps every decision at 9.2
 // sigma; the last one takes the rest.
@@ -315,7 +325,7 @@ static int sign_schedule(const fhe_params& p, int* d_out, int* sched) {
   }
   int lad[NGAD], m = 0;
   lad[m++] = 0;
-  for (int g : {3, 4, 1, 2})
+  for (int g : {5, 3, 4, 1, 2})
     if (gadget_level(p, g)) lad[m++] = g;
   const int first = p.sign_digit_bits ? std::min(p.sign_digit_bits, P) : std::min(4, P);
   const int last = p.sign_digit_bits ? first : 3;
@@ -496,6 +506,7 @@ void fhe_ctx_destroy(fhe_ctx* ctx) {
                       (void*)ctx->ksk_colsum, (void*)ctx->bsk_fft, (void*)ctx->tw, (void*)ctx->twist, ctx->ws,
                       (void*)ctx->bskf[0], (void*)ctx->bskf[1], (void*)ctx->bskf_fft[0], (void*)ctx->bskf_fft[1],
                       (void*)ctx->bskf[2], (void*)ctx->bskf[3], (void*)ctx->bskf_fft[2], (void*)ctx->bskf_fft[3],
+                      (void*)ctx->bskf[4], (void*)ctx->bskf_fft[4],
                       (void*)ctx->ksk8, (void*)ctx->ks_ws, (void*)ctx->ks_ws1, (void*)ctx->tw4, (void*)ctx->bsk_fft_v2,
                       (void*)ctx->psi, (void*)ctx->mb_msg})
       (void)hipFree(ptr);
@@ -554,7 +565,7 @@ static int variant_for(const fhe_ctx* ctx, const fhe_params& q) {
   return ctx->br_variant;
 }
 // the parameters seen through gadget g (1: pbs_fast_*, 2: pbs_fast2_*, 3:
-// pbs_mid_*, 4: pbs_mid2_*; same secret keys, other decomposition and
+// pbs_mid_*, 4: pbs_mid2_*, 5: pbs_mid0_*; same secret keys, other decomposition and
 // bootstrapping key)
 static int fast_level(const fhe_params& p, int g) { return g >= 1 && g < NGAD ? gadget_level(p, g) : 0; }
 // fast gadget g runs the multi-bit blind rotation
@@ -575,13 +586,15 @@ size_t fhe_fast_bsk_words(const fhe_params* p, int32_t which) {
   return fast_bsk_words(*p, which);
 }
 // the other gadgets' keys under the ChaCha20 streams 9/10 (fast), 11/12
-// (fast2), 17/18 (mid) and 19/20 (mid2); 13/14, 15/16, 21/22 and 23/24 for
-// the fast, fast2, mid and mid2 gadgets' multi-bit keys, whose GGSW messages
+// (fast2), 17/18 (mid), 19/20 (mid2) and 25/26 (mid0); 13/14, 15/16, 21/22,
+// 23/24 and 27/28 for those gadgets' multi-bit keys, whose GGSW messages
 // k_mb_msgs derives
-static const uint32_t kTagMask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK};
-static const uint32_t kTagNoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE};
-static const uint32_t kTagMbMask[NGAD] = {0, TAG_MB2_MASK, TAG_MB3_MASK, TAG_MB4_MASK, TAG_MB5_MASK};
-static const uint32_t kTagMbNoise[NGAD] = {0, TAG_MB2_NOISE, TAG_MB3_NOISE, TAG_MB4_NOISE, TAG_MB5_NOISE};
+static const uint32_t kTagMask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK,
+                                        TAG_BSK6_MASK};
+static const uint32_t kTagNoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE,
+                                         TAG_BSK6_NOISE};
+static const uint32_t kTagMbMask[NGAD] = {0, TAG_MB2_MASK, TAG_MB3_MASK, TAG_MB4_MASK, TAG_MB5_MASK, TAG_MB6_MASK};
+static const uint32_t kTagMbNoise[NGAD] = {0, TAG_MB2_NOISE, TAG_MB3_NOISE, TAG_MB4_NOISE, TAG_MB5_NOISE, TAG_MB6_NOISE};
 static void keygen_fast_bsks(fhe_ctx* ctx, const ChaKey& K, hipStream_t st) {
   const fhe_params& p = ctx->p;
   const size_t shm = 8 * (size_t)p.N + p.N;
@@ -710,7 +723,7 @@ int fhe_export_fast_bsk(fhe_ctx* ctx, int32_t which, uint64_t* h_bsk) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   if (which < 1 || which >= NGAD)
-    return fail(ctx, FHE_E_ARG, "which must be 1 (fast), 2 (fast2), 3 (mid) or 4 (mid2)");
+    return fail(ctx, FHE_E_ARG, "which must be 1 (fast), 2 (fast2), 3 (mid), 4 (mid2) or 5 (mid0)");
   if (!fast_level(ctx->p, which)) return fail(ctx, FHE_E_STATE, "no such fast gadget in these parameters");
   if (!h_bsk) return fail(ctx, FHE_E_ARG, "null buffer");
   const fhe_params q = fast_params(ctx->p, which);
@@ -1846,6 +1859,7 @@ static ProfAcc* prof_bucket(fhe_ctx* ctx, const char* kernel) {
   if (!strcmp(kernel, "blind_rotate_fast2")) return &ctx->prof_brf[1];
   if (!strcmp(kernel, "blind_rotate_mid")) return &ctx->prof_brf[2];
   if (!strcmp(kernel, "blind_rotate_mid2")) return &ctx->prof_brf[3];
+  if (!strcmp(kernel, "blind_rotate_mid0")) return &ctx->prof_brf[4];
   if (!strcmp(kernel, "keyswitch")) return &ctx->prof_ks;
   if (!strcmp(kernel, "encrypt_linear")) return &ctx->prof_enc;
   return nullptr;
@@ -1873,7 +1887,7 @@ int fhe_profile_read(fhe_ctx* ctx, const char* kernel, double* total_ms, int64_t
   if (!kernel) return fail(ctx, FHE_E_ARG, "null kernel name");
   std::vector<ProfAcc*> acc;
   if (!strcmp(kernel, "blind_rotate"))
-    acc = {&ctx->prof_br, &ctx->prof_brf[0], &ctx->prof_brf[1], &ctx->prof_brf[2], &ctx->prof_brf[3]};
+    acc = {&ctx->prof_br, &ctx->prof_brf[0], &ctx->prof_brf[1], &ctx->prof_brf[2], &ctx->prof_brf[3], &ctx->prof_brf[4]};
   else if (ProfAcc* a = prof_bucket(ctx, kernel)) acc = {a};
   else return fail(ctx, FHE_E_ARG, "unknown kernel name");
   double ms = 0;

@@ -37,6 +37,10 @@ enum StreamTag : uint32_t {
   TAG_MB4_NOISE = 22,
   TAG_MB5_MASK = 23,   // the mid2 gadget's multi-bit key
   TAG_MB5_NOISE = 24,
+  TAG_BSK6_MASK = 25,  // the mid0 gadget's bootstrapping key (fhe_params.pbs_mid0_*)
+  TAG_BSK6_NOISE = 26,
+  TAG_MB6_MASK = 27,   // the mid0 gadget's multi-bit key
+  TAG_MB6_NOISE = 28,
 };
 
 struct ChaKey {

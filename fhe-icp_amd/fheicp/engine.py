@@ -96,10 +96,10 @@ class Engine:
 
     def export_fast_bsk(self, which: int = 1) -> np.ndarray:
         """Another gadget's bootstrapping key (which = 1: params.pbs_fast_*,
-        2: pbs_fast2_*, 3: pbs_mid_*, 4: pbs_mid2_*)."""
+        2: pbs_fast2_*, 3: pbs_mid_*, 4: pbs_mid2_*, 5: pbs_mid0_*)."""
         from .params import gadget_level
         p = self.params
-        if which not in (1, 2, 3, 4) or not gadget_level(p, which):
+        if which not in (1, 2, 3, 4, 5) or not gadget_level(p, which):
             raise ValueError(f"these parameters have no fast gadget {which}")
         q = _lib.params_struct(p.as_dict())
         out = np.zeros(self._L.fhe_fast_bsk_words(C.byref(q), which), np.uint64)

@@ -61,6 +61,13 @@ class SchemeParams:
     # pbs_fast_group; 2 = multi-bit, 48-bit accumulators past level 2)
     pbs_mid_group: int = 0
     pbs_mid2_group: int = 0
+    # a sixth gadget between the main and the mid one (0, 0 = none; needs
+    # mid): the ladder is main -> mid0 -> mid -> mid2 -> fast -> fast2, so a
+    # plan's most amplified round can run on a multi-bit gadget as precise as
+    # the classic main one (P = 26: (5,8) multi-bit)
+    pbs_mid0_base_log: int = 0
+    pbs_mid0_level: int = 0
+    pbs_mid0_group: int = 0
 
     def as_dict(self) -> dict:
         return asdict(self)
@@ -112,18 +119,19 @@ def sign_rounds(P: int, d: int):
     return out
 
 
-# gadget ids (fhe_pbs_gadget_batch): 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2
-GADGET_IDS = (0, 1, 2, 3, 4)
+# gadget ids (fhe_pbs_gadget_batch): 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2, 5 mid0
+GADGET_IDS = (0, 1, 2, 3, 4, 5)
 
 
 def gadget_level(p: "SchemeParams", g: int) -> int:
-    return (p.pbs_level, p.pbs_fast_level, p.pbs_fast2_level, p.pbs_mid_level, p.pbs_mid2_level)[g]
+    return (p.pbs_level, p.pbs_fast_level, p.pbs_fast2_level, p.pbs_mid_level, p.pbs_mid2_level,
+            p.pbs_mid0_level)[g]
 
 
 def gadget_of(p: "SchemeParams", g: int):
     """(base_log, level, group) of gadget g: 0 main, 1 fast, 2 fast2, 3 mid,
-    4 mid2 (an absent fast2 falls back to the fast one, an absent fast, mid or
-    mid2 gadget to the main one)."""
+    4 mid2, 5 mid0 (an absent fast2 falls back to the fast one, an absent
+    fast, mid, mid2 or mid0 gadget to the main one)."""
     if g == 2 and p.pbs_fast2_level:
         return p.pbs_fast2_base_log, p.pbs_fast2_level, max(p.pbs_fast2_group, 1)
     if g in (1, 2) and p.pbs_fast_level:
@@ -132,6 +140,8 @@ def gadget_of(p: "SchemeParams", g: int):
         return p.pbs_mid_base_log, p.pbs_mid_level, max(p.pbs_mid_group, 1)
     if g == 4 and p.pbs_mid2_level:
         return p.pbs_mid2_base_log, p.pbs_mid2_level, max(p.pbs_mid2_group, 1)
+    if g == 5 and p.pbs_mid0_level:
+        return p.pbs_mid0_base_log, p.pbs_mid0_level, max(p.pbs_mid0_group, 1)
     return p.pbs_base_log, p.pbs_level, 1
 
 
@@ -166,9 +176,9 @@ def _plan_worst(p: "SchemeParams", d: int, j1: int, j2: int | None = None) -> fl
 
 
 def _ladder(p: "SchemeParams"):
-    """The gadgets the sign plan walks through, in order: main, mid, mid2,
-    fast, fast2 (those present)."""
-    return [0] + [g for g in (3, 4, 1, 2) if gadget_level(p, g)]
+    """The gadgets the sign plan walks through, in order: main, mid0, mid,
+    mid2, fast, fast2 (those present)."""
+    return [0] + [g for g in (5, 3, 4, 1, 2) if gadget_level(p, g)]
 
 
 def sign_schedule(p: "SchemeParams"):
@@ -300,6 +310,27 @@ def _cheapest_plan(p: SchemeParams) -> SchemeParams:
     return p
 
 
+def _with_mid0(p: SchemeParams) -> SchemeParams:
+    """p with a sixth gadget ahead of the mids if it makes the plan cheaper:
+    a multi-bit one above the mid level, up to one past the main gadget's
+    (its more precise neighbour in PBS_GADGETS), with L * beta <= 47 (the
+    48-bit-accumulator kernels), so the first, most amplified rounds run on
+    the multi-bit rotation instead of the classic main one.
+    Tried after the main gadget is chosen, so plans it does not improve stay
+    as they were."""
+    if not p.pbs_mid_level:
+        return p
+    best, q1 = plan_cost(p), p
+    for b0, lv0 in sorted({(b, lv) for _, b, lv in PBS_GADGETS if p.pbs_mid_level < lv <= q1.pbs_level + 1}):
+        if (lv0, 2) not in BR_COST or b0 * lv0 > 47:
+            continue
+        q = replace(q1, pbs_mid0_base_log=b0, pbs_mid0_level=lv0, pbs_mid0_group=2)
+        c = plan_cost(q)
+        if c < best - 1e-9:
+            p, best = q, c
+    return p
+
+
 def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
     """The gadget of PBS_GADGETS for width P; with fast, also up to two of
     FAST_GADGETS (other than the main gadget, in their order: fast, then
@@ -309,7 +340,7 @@ def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
     rounds between, if they make the plan cheaper still. A more precise main
     gadget (the next entry of the table) is taken when its cheapest plan is
     cheaper: a quieter first bootstrap can allow 4-bit digits (DESIGN.md
-    §3.6)."""
+    §3.6). Last, a multi-bit mid0 gadget for the first rounds (_with_mid0)."""
     for i, (pmax, beta, lvl) in enumerate(PBS_GADGETS):
         if P <= pmax:
             p = SchemeParams(pbs_base_log=beta, pbs_level=lvl, msg_bits=P)
@@ -322,7 +353,7 @@ def params_for_bits(P: int, fast: bool = True) -> SchemeParams:
                 c = plan_cost(q)
                 if c < best - 1e-9:
                     p, best = q, c
-            return p
+            return _with_mid0(p)
     raise ValueError(f"accumulator width P={P} exceeds the supported 27 bits")
 
 

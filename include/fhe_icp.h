@@ -83,6 +83,13 @@ typedef struct fhe_params {
   int32_t pbs_mid2_group;    /* rotation, as pbs_fast_group: 2 = multi-bit (levels
                                 up to 8; 48-bit accumulators past level 2 or
                                 level * base_log > 31: k_blind_rotate_mb64) */
+  int32_t pbs_mid0_base_log; /* optional sixth gadget between the main and the mid */
+  int32_t pbs_mid0_level;    /* one (0, 0: none; needs mid): the ladder is main ->  */
+  int32_t pbs_mid0_group;    /* mid0 -> mid -> mid2 -> fast -> fast2, so a plan can run
+                                its most amplified round on a multi-bit gadget as
+                                precise as the classic main one (P = 26: (5,8)
+                                multi-bit). Key: fhe_export_fast_bsk
+                                which = 5 (stream tags 25/26, 27/28 multi-bit). */
 } fhe_params;
 
 typedef struct fhe_ctx fhe_ctx;
@@ -123,7 +130,8 @@ int fhe_import_keys(fhe_ctx* ctx, const uint64_t* h_s_small, const uint64_t* h_s
                     const uint64_t* h_ksk);
 /* a fast gadget's bootstrapping key, which = 1 (pbs_fast_*, stream tags
  * 9/10, or 13/14 for a multi-bit key), 2 (pbs_fast2_*, tags 11/12 or
- * 15/16), 3 (pbs_mid_*, tags 17/18) or 4 (pbs_mid2_*, tags 19/20): the
+ * 15/16), 3 (pbs_mid_*, tags 17/18), 4 (pbs_mid2_*, tags 19/20) or 5
+ * (pbs_mid0_*, tags 25/26; 21/22, 23/24 and 27/28 multi-bit): the
  * layout of bsk with one GGSW per LWE coefficient, or three per
  * pair of coefficients ([pair][subset {1}, {2}, {1,2}][row][component][coef])
  * when that gadget's group is 2; fhe_fast_bsk_words words (0: no such
@@ -191,7 +199,7 @@ int fhe_pbs_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint64_t
                   void* stream);
 /* fhe_pbs_batch on one of the parameter set's gadgets: 0 = the main one
  * (pbs_base_log, pbs_level), 1 = pbs_fast_*, 2 = pbs_fast2_*, 3 = pbs_mid_*,
- * 4 = pbs_mid2_* (with their own
+ * 4 = pbs_mid2_*, 5 = pbs_mid0_* (with their own
  * bootstrapping keys and kernels, e.g. the multi-bit rotation of
  * pbs_fast_group = 2). FHE_E_STATE if that gadget is
  * absent. */
@@ -222,7 +230,7 @@ int fhe_sign_precise_rounds(const fhe_params* params);
  * order, fhe_sign_schedule), the rest on fast2
  * (DESIGN.md §3.6). Any pointer may be NULL. */
 int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_rounds, int32_t* fast_end);
-/* the gadget (0..4, as fhe_pbs_gadget_batch) of every bootstrap of
+/* the gadget (0..5, as fhe_pbs_gadget_batch) of every bootstrap of
  * fhe_sign_batch in order, into gadgets[0 .. min(R, cap)); returns R (the
  * bootstraps per sign extraction) or FHE_E_ARG on bad params. */
 int fhe_sign_schedule(const fhe_params* params, int32_t* gadgets, int32_t cap);
@@ -360,7 +368,7 @@ int fhe_stream_sync(fhe_ctx* ctx, void* stream);
  * synchronises and returns total milliseconds, launch count and ciphertexts
  * processed for kernel "blind_rotate" (all gadgets), "blind_rotate_main",
  * "blind_rotate_fast" (fhe_params.pbs_fast_*), "blind_rotate_fast2",
- * "blind_rotate_mid", "blind_rotate_mid2", "keyswitch" or "encrypt_linear"
+ * "blind_rotate_mid", "blind_rotate_mid2", "blind_rotate_mid0", "keyswitch" or "encrypt_linear"
  * (the fused client encryption + leveled dot), then resets what it
  * read. */
 int fhe_profile_enable(fhe_ctx* ctx, int enable);

@@ -25,7 +25,8 @@ FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
           "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
           "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
           "pbs_fast_group", "pbs_fast2_group", "pbs_mid_base_log", "pbs_mid_level", "pbs_mid2_base_log",
-          "pbs_mid2_level", "pbs_mid_group", "pbs_mid2_group")
+          "pbs_mid2_level", "pbs_mid_group", "pbs_mid2_group", "pbs_mid0_base_log", "pbs_mid0_level",
+          "pbs_mid0_group")
 
 
 class fhe_params(C.Structure):

@@ -57,6 +57,9 @@ typedef struct {
   int32_t pbs_mid2_level;
   int32_t pbs_mid_group;      /* blind rotation of the mid / mid2 gadget    */
   int32_t pbs_mid2_group;     /* (as pbs_fast_group)                        */
+  int32_t pbs_mid0_base_log;  /* sixth gadget, between the main and the mid */
+  int32_t pbs_mid0_level;     /* one (0, 0 = none; needs mid)               */
+  int32_t pbs_mid0_group;
 } ref_params;
 
 /* --------------------------------------------------------------- chacha --- */
@@ -138,7 +141,8 @@ enum { TAG_SK_SMALL = 1, TAG_SK_GLWE = 2, TAG_BSK_MASK = 3, TAG_BSK_NOISE = 4, T
        TAG_KSK_NOISE = 6, TAG_ENC_MASK = 7, TAG_ENC_NOISE = 8, TAG_BSK2_MASK = 9, TAG_BSK2_NOISE = 10,
        TAG_BSK3_MASK = 11, TAG_BSK3_NOISE = 12, TAG_MB2_MASK = 13, TAG_MB2_NOISE = 14, TAG_MB3_MASK = 15,
        TAG_MB3_NOISE = 16, TAG_BSK4_MASK = 17, TAG_BSK4_NOISE = 18, TAG_BSK5_MASK = 19, TAG_BSK5_NOISE = 20,
-       TAG_MB4_MASK = 21, TAG_MB4_NOISE = 22, TAG_MB5_MASK = 23, TAG_MB5_NOISE = 24 };
+       TAG_MB4_MASK = 21, TAG_MB4_NOISE = 22, TAG_MB5_MASK = 23, TAG_MB5_NOISE = 24, TAG_BSK6_MASK = 25,
+       TAG_BSK6_NOISE = 26, TAG_MB6_MASK = 27, TAG_MB6_NOISE = 28 };
 
 /* --------------------------------------------------- negacyclic product --- */
 /* c[0..2n-2] = a * b (plain product over Z_{2^64}); scratch >= 4n words */
@@ -225,11 +229,12 @@ static void bsk_gen(const ref_params* P, const ref_key* Kp, int beta, int L, int
  * of s1(1-s2), (1-s1)s2 and s1 s2 (the subsets {1}, {2}, {1,2}). */
 static int gadget_group(const ref_params* P, int which) {
   const int g = which == 1 ? P->pbs_fast_group : which == 2 ? P->pbs_fast2_group
-              : which == 3 ? P->pbs_mid_group : which == 4 ? P->pbs_mid2_group : 1;
+              : which == 3 ? P->pbs_mid_group : which == 4 ? P->pbs_mid2_group
+              : which == 5 ? P->pbs_mid0_group : 1;
   return g == 2 ? 2 : 1;
 }
-/* gadget `which`: 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2 (level 0: absent) */
-#define NGAD 5
+/* gadget `which`: 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2, 5 mid0 (level 0: absent) */
+#define NGAD 6
 static int gadget_level(const ref_params* P, int which) {
   switch (which) {
     case 0: return P->pbs_level;
@@ -237,6 +242,7 @@ static int gadget_level(const ref_params* P, int which) {
     case 2: return P->pbs_fast2_level;
     case 3: return P->pbs_mid_level;
     case 4: return P->pbs_mid2_level;
+    case 5: return P->pbs_mid0_level;
   }
   return 0;
 }
@@ -247,6 +253,7 @@ static int gadget_base_log(const ref_params* P, int which) {
     case 2: return P->pbs_fast2_base_log;
     case 3: return P->pbs_mid_base_log;
     case 4: return P->pbs_mid2_base_log;
+    case 5: return P->pbs_mid0_base_log;
   }
   return 0;
 }
@@ -276,13 +283,15 @@ int ref_keygen_fast_bsk(const ref_params* P, uint64_t seed, int which, const uin
   ref_key K;
   key_from_seed(seed, &K);
   const int bl = gadget_base_log(P, which);
-  static const int tmask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK};
-  static const int tnoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE};
+  static const int tmask[NGAD] = {TAG_BSK_MASK, TAG_BSK2_MASK, TAG_BSK3_MASK, TAG_BSK4_MASK, TAG_BSK5_MASK,
+                                  TAG_BSK6_MASK};
+  static const int tnoise[NGAD] = {TAG_BSK_NOISE, TAG_BSK2_NOISE, TAG_BSK3_NOISE, TAG_BSK4_NOISE, TAG_BSK5_NOISE,
+                                   TAG_BSK6_NOISE};
   if (gadget_group(P, which) == 2) {
     uint64_t* msg = (uint64_t*)malloc(8 * 3 * (size_t)npairs(P));
     mb_msgs(P, s_small, msg);
-    static const int mmask[NGAD] = {0, TAG_MB2_MASK, TAG_MB3_MASK, TAG_MB4_MASK, TAG_MB5_MASK};
-    static const int mnoise[NGAD] = {0, TAG_MB2_NOISE, TAG_MB3_NOISE, TAG_MB4_NOISE, TAG_MB5_NOISE};
+    static const int mmask[NGAD] = {0, TAG_MB2_MASK, TAG_MB3_MASK, TAG_MB4_MASK, TAG_MB5_MASK, TAG_MB6_MASK};
+    static const int mnoise[NGAD] = {0, TAG_MB2_NOISE, TAG_MB3_NOISE, TAG_MB4_NOISE, TAG_MB5_NOISE, TAG_MB6_NOISE};
     bsk_gen(P, &K, bl, L, mmask[which], mnoise[which], msg, 3 * npairs(P), s_big, bsk2);
     free(msg);
   } else {
@@ -957,9 +966,9 @@ static int sign_schedule(const ref_params* P, int* d_out, int* sched) {
   int dd = 3;
   if (P->pbs_fast_level) {
     int lad[NGAD], m = 0;
-    const int order[4] = {3, 4, 1, 2};
+    const int order[5] = {5, 3, 4, 1, 2};
     lad[m++] = 0;
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 5; ++i)
       if (gadget_level(P, order[i])) lad[m++] = order[i];
     const int first = P->sign_digit_bits ? (P->sign_digit_bits < Pb ? P->sign_digit_bits : Pb) : d4;
     const int last = P->sign_digit_bits ? first : 3;
@@ -1010,7 +1019,7 @@ static int digit_bits(const ref_params* P) {
 /* the bootstrap gadget and key of the next round (sign_schedule) */
 typedef struct {
   const ref_params* P;
-  ref_params Pf[NGAD - 1]; /* P seen through gadget 1..4 */
+  ref_params Pf[NGAD - 1]; /* P seen through gadget 1..5 */
   const uint64_t* bsk[NGAD];
   int sched[64];
   int r;
@@ -1043,8 +1052,8 @@ static void digit_rounds(gadget_sched* g, const uint64_t* ksk, uint64_t* cv, int
  * digits [b, b+d) by digit_rounds, a leftover of >= 3 bits as one shorter
  * digit, of 1-2 bits by single-bit rounds; then the sign of the top d bits
  * (centred by 2^(63-d), tv 2^62). sign[count x (kN+1)] encrypts [v < 0] at
- * 2^63; ct_v is consumed. keys[g - 1] is the key of gadget g = 1..4 (fast,
- * fast2, mid, mid2); round r runs on gadget sign_schedule[r]; a NULL key
+ * 2^63; ct_v is consumed. keys[g - 1] is the key of gadget g = 1..5 (fast,
+ * fast2, mid, mid2, mid0); round r runs on gadget sign_schedule[r]; a NULL key
  * plans as if that gadget were not set (with the ones that need it). */
 void ref_sign_extract_keys(const ref_params* P0, const uint64_t* bsk, const uint64_t* const* keys,
                            const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
@@ -1053,6 +1062,7 @@ void ref_sign_extract_keys(const ref_params* P0, const uint64_t* bsk, const uint
   if (!keys[0] || !keys[1]) Pm.pbs_fast2_base_log = Pm.pbs_fast2_level = Pm.pbs_fast2_group = 0;
   if (!keys[0] || !keys[2]) Pm.pbs_mid_base_log = Pm.pbs_mid_level = Pm.pbs_mid_group = 0;
   if (!Pm.pbs_mid_level || !keys[3]) Pm.pbs_mid2_base_log = Pm.pbs_mid2_level = Pm.pbs_mid2_group = 0;
+  if (!Pm.pbs_mid_level || !keys[4]) Pm.pbs_mid0_base_log = Pm.pbs_mid0_level = Pm.pbs_mid0_group = 0;
   const ref_params* P = &Pm;
   const int Wb = P->k * P->N + 1, Pb = P->msg_bits;
   gadget_sched g0;

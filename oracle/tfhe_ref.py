@@ -19,10 +19,12 @@ FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
           "lwe_noise_bits", "glwe_noise_bits", "msg_bits", "sign_digit_bits",
           "pbs_fast_base_log", "pbs_fast_level", "pbs_fast2_base_log", "pbs_fast2_level",
           "pbs_fast_group", "pbs_fast2_group", "pbs_mid_base_log", "pbs_mid_level", "pbs_mid2_base_log",
-          "pbs_mid2_level", "pbs_mid_group", "pbs_mid2_group")
+          "pbs_mid2_level", "pbs_mid_group", "pbs_mid2_group", "pbs_mid0_base_log", "pbs_mid0_level",
+          "pbs_mid0_group")
 OPTIONAL = FIELDS[FIELDS.index("sign_digit_bits"):]
-# gadget g = 1..4 (fast, fast2, mid, mid2) and the level field that enables it
-GADGET_LEVEL = {1: "pbs_fast_level", 2: "pbs_fast2_level", 3: "pbs_mid_level", 4: "pbs_mid2_level"}
+# gadget g = 1..5 (fast, fast2, mid, mid2, mid0) and the level field that enables it
+GADGET_LEVEL = {1: "pbs_fast_level", 2: "pbs_fast2_level", 3: "pbs_mid_level", 4: "pbs_mid2_level",
+                5: "pbs_mid0_level"}
 
 
 class RefParams(C.Structure):
@@ -117,7 +119,7 @@ class RefTFHE:
         L.ref_keygen(C.byref(self.P), C.c_uint64(seed), u64(self.s_small), u64(self.s_big), u64(self.bsk),
                      u64(self.ksk))
         # the other gadgets' bootstrapping keys (fhe_keygen generates them
-        # too): keys[g] for g = 1..4 (fast, fast2, mid, mid2)
+        # too): keys[g] for g = 1..5 (fast, fast2, mid, mid2, mid0)
         self.keys = {}
         for which, lv in GADGET_LEVEL.items():
             if self.params[lv]:
@@ -278,7 +280,7 @@ class RefTFHE:
         cv = np.array(ct_v, dtype=np.uint64, copy=True, order="C")
         cnt = cv.size // (self.big + 1)
         sign = np.zeros((cnt, self.big + 1), np.uint64)
-        keys = (C.POINTER(C.c_uint64) * 4)(*[u64(self.keys[g]) if g in self.keys else None for g in range(1, 5)])
+        keys = (C.POINTER(C.c_uint64) * 5)(*[u64(self.keys[g]) if g in self.keys else None for g in range(1, 6)])
         lib().ref_sign_extract_keys(C.byref(self.P), u64(self.bsk), keys, u64(self.ksk), u64(cv), cnt, u64(sign))
         return sign
 
@@ -353,7 +355,7 @@ def sign_plan(params: dict):
 
 
 def sign_schedule(params: dict) -> list:
-    """The gadget (0 main, 1 fast, 2 fast2, 3 mid, 4 mid2) of every bootstrap
+    """The gadget (0 main, 1 fast, 2 fast2, 3 mid, 4 mid2, 5 mid0) of every bootstrap
     of the sign extraction (ref_sign_schedule)."""
     out = (C.c_int32 * 64)()
     R = lib().ref_sign_schedule(C.byref(_ref_params(params)), out, 64)

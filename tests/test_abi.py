@@ -119,7 +119,7 @@ def test_build_info_and_kernel_names_on_host_context():
     assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
     buf = C.create_string_buffer(64)
     for k in (b"blind_rotate", b"blind_rotate_main", b"blind_rotate_fast", b"blind_rotate_fast2",
-              b"blind_rotate_mid", b"blind_rotate_mid2", b"keyswitch"):
+              b"blind_rotate_mid", b"blind_rotate_mid2", b"blind_rotate_mid0", b"keyswitch"):
         assert L.fhe_profile_kernel_name(h, k, buf, 64) == 0 and buf.value == b""
     assert L.fhe_profile_kernel_name(h, b"nope", buf, 64) == -1
     assert L.fhe_profile_kernel_name(h, b"keyswitch", None, 64) == -1
@@ -132,16 +132,21 @@ def test_build_info_and_kernel_names_on_host_context():
 
 def test_mid_gadget_validation_and_schedule(oracle_lib):
     """The mid-gadget fields: each pair all-or-nothing, mid needs the fast
-    gadget, mid2 needs mid; fhe_sign_schedule fills at most cap entries and
-    returns R; the mid keys' sizes (which = 3, 4) equal the oracle's."""
+    gadget, mid2 and mid0 need mid; fhe_sign_schedule fills at most cap
+    entries and returns R; the mid keys' sizes (which = 3, 4, 5) equal the
+    oracle's."""
     from fheicp.params import sign_schedule
     L = _lib.lib()
     h = C.c_void_p()
     base = params_for_bits(26).as_dict()
-    assert base["pbs_mid_level"] and base["pbs_mid2_level"]
+    assert base["pbs_mid_level"] and base["pbs_mid2_level"] and base["pbs_mid0_level"]
     for bad, why in ((dict(base, pbs_mid_level=0), b"mid pbs"),
                      (dict(base, pbs_mid_base_log=0, pbs_mid_level=0), b"mid2"),
                      (dict(base, pbs_mid2_base_log=0), b"mid2"),
+                     (dict(base, pbs_mid0_level=0), b"mid0"),
+                     (dict(base, pbs_mid0_group=3), b"pbs_mid0_group"),
+                     (dict(base, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid2_base_log=0, pbs_mid2_level=0),
+                      b"mid0"),
                      (dict(base, pbs_fast_base_log=0, pbs_fast_level=0, pbs_fast2_base_log=0, pbs_fast2_level=0),
                       b"mid pbs")):
         P = _lib.params_struct(bad)
@@ -156,9 +161,9 @@ def test_mid_gadget_validation_and_schedule(oracle_lib):
     assert L.fhe_sign_schedule(C.byref(P), out, 3) == R and list(out) == want[:3] + [-1]
     ol = oracle_lib.lib()
     RP = oracle_lib.RefParams(**base)
-    for which in (1, 2, 3, 4):
+    for which in (1, 2, 3, 4, 5):
         assert L.fhe_fast_bsk_words(C.byref(P), which) == ol.ref_bsk2_words(C.byref(RP), which) > 0, which
-    assert L.fhe_fast_bsk_words(C.byref(P), 5) == 0
+    assert L.fhe_fast_bsk_words(C.byref(P), 6) == 0
     assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
     buf = (C.c_uint64 * 1)()
     assert L.fhe_export_fast_bsk(h, 3, buf) == -2
@@ -182,7 +187,7 @@ def test_bert_abi_validation():
 
 
 def test_gadget_group_validation():
-    """Every gadget's grouping factor (fast, fast2, mid, mid2) is 0, 1 or 2,
+    """Every gadget's grouping factor (fast, fast2, mid, mid2, mid0) is 0, 1 or 2,
     and a multi-bit (group 2) gadget needs N = 1024, k = 2, n <= 1023 and
     level <= 8 (the 48-bit-accumulator kernels go to level 8); the oracle
     library resolves the same plan for the planner's multi-bit mids."""
@@ -194,7 +199,7 @@ def test_gadget_group_validation():
     P = _lib.params_struct(p21.as_dict())
     assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
     L.fhe_ctx_destroy(h)
-    for field in ("pbs_fast_group", "pbs_fast2_group", "pbs_mid_group", "pbs_mid2_group"):
+    for field in ("pbs_fast_group", "pbs_fast2_group", "pbs_mid_group", "pbs_mid2_group", "pbs_mid0_group"):
         P = _lib.params_struct(dict(p21.as_dict(), **{field: 3}))
         assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == -1, field
         assert b"must be 0, 1 or 2" in L.fhe_last_error(None)

@@ -40,7 +40,7 @@ def test_estimator_threshold_bit(fitted):
 
 
 def _br_totals(eng):
-    gs = ("main", "mid", "mid2", "fast", "fast2")
+    gs = ("main", "mid0", "mid", "mid2", "fast", "fast2")
     rd = {g: eng.profile_read(f"blind_rotate_{g}") for g in gs}
     return (sum(r["launches"] for r in rd.values()), sum(r["items"] for r in rd.values()),
             eng.profile_read("keyswitch")["launches"])

@@ -257,7 +257,8 @@ TOY_FAST = dict(pbs_base_log=12, pbs_level=3, pbs_fast_base_log=8, pbs_fast_leve
 def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
     """Every bootstrapping key of a multi-gadget parameter set (toy (12,3)+(8,2);
     real P=16: (15,2) + (15,2) + (23,1); P=19: (12,3) + mid (12,3) + (15,2) +
-    (23,1); P=26: (5,8) + mid (8,5) + mid2 (12,3) + (15,2) + (23,1)) is
+    (23,1); P=26: (6,7) + mid0 (5,8) + mid (8,5) + mid2 (12,3) + (15,2) +
+    (23,1)) is
     bit-exact against the oracle's keygen, the fast gadgets' keys as
     multi-bit keys (group 2: three GGSWs per pair) and as classic ones, the
     mid gadgets' as the planner sets them (multi-bit)."""
@@ -272,25 +273,31 @@ def test_fast_bsk_bit_exact(need_gpu, oracle_lib, P, grp):
     assert np.array_equal(eng.export_fast_bsk(1), ref.bsk2)
     if prm.pbs_fast2_level:
         assert np.array_equal(eng.export_fast_bsk(2), ref.bsk3)
-    for which in (3, 4):
+    for which in (3, 4, 5):
         if which in ref.keys:
             assert np.array_equal(eng.export_fast_bsk(which), ref.keys[which]), which
     assert (3 in ref.keys) == (P >= 17)   # multi-bit mid keys (tags 21-24) from P = 17
+    assert (5 in ref.keys) == (P >= 25)   # the multi-bit mid0 key (tags 27-28) from P = 25
     eng.close()
 
 
-@pytest.mark.parametrize("P,dbits,mid2", [(11, 4, None), (11, 3, (9, 2))])
-def test_sign_toy_mid_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits, mid2):
-    """Mid gadgets (toy main (12,3) -> mid (10,2) [-> mid2 (9,2)] -> fast
-    (8,2) -> fast2 (11,1)): the schedule puts rounds on every key, the mid keys
-    are bit-exact, every value keeps its sign and the phases track the
-    oracle's five-key restatement."""
+@pytest.mark.parametrize("P,dbits,mid2,mid0", [(11, 4, None, None), (11, 3, (9, 2), None),
+                                               (11, 3, (9, 2), (11, 3))])
+def test_sign_toy_mid_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits, mid2, mid0):
+    """Mid gadgets (toy main (12,3) [-> mid0 (11,3)] -> mid (10,2) [-> mid2
+    (9,2)] -> fast (8,2) -> fast2 (11,1)): the schedule puts rounds on every
+    key (with mid0, on all but the main one), the mid keys are bit-exact,
+    every value keeps its sign and the phases track the oracle's six-key
+    restatement."""
     from fheicp.params import sign_schedule
     kw = dict(TOY_FAST3, pbs_mid_base_log=10, pbs_mid_level=2)
     if mid2:
         kw.update(pbs_mid2_base_log=mid2[0], pbs_mid2_level=mid2[1])
+    if mid0:
+        kw.update(pbs_mid0_base_log=mid0[0], pbs_mid0_level=mid0[1])
     prm = replace(TOY, msg_bits=P, sign_digit_bits=dbits, **kw)
-    assert set(sign_schedule(prm)[1]) == ({0, 1, 2, 3, 4} if mid2 else {0, 1, 2, 3})
+    want = {5, 1, 2, 3, 4} if mid0 else {0, 1, 2, 3, 4} if mid2 else {0, 1, 2, 3}
+    assert set(sign_schedule(prm)[1]) == want
     eng = Engine(prm, 0)
     eng.keygen(4324)
     ref = oracle_lib.RefTFHE(prm.as_dict(), 4324)

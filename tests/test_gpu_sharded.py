@@ -56,7 +56,7 @@ def _rank_main(rank, world, port, store_dir, query, cases, q):
         res = [p.search_vector(np.asarray(query), k, t) for k, t in cases]
         torch.cuda.synchronize()
         eng.profile(False)
-        brs = {g: eng.profile_read(f"blind_rotate_{g}")["items"] for g in ("main", "mid", "mid2", "fast", "fast2")}
+        brs = {g: eng.profile_read(f"blind_rotate_{g}")["items"] for g in ("main", "mid0", "mid", "mid2", "fast", "fast2")}
         from fheicp.params import sign_pbs_count
         brs["per_compare"] = sign_pbs_count(eng.params)
         q.put((rank, res, p.fhe_model.model.quant_params.to_dict(), brs, _lib.LIB_PATH and str(_lib.LIB_PATH)))

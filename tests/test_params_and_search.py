@@ -129,7 +129,7 @@ def test_mid_gadget_plan():
         assert got2 == m2, P
         d, sched = sign_schedule(p)
         assert len(sched) == sign_pbs_count(p) and _sched_worst(p, d, sched) >= 9.2, P
-        lad = [g for g in (0, 3, 4, 1, 2) if g in sched]
+        lad = [g for g in (0, 5, 3, 4, 1, 2) if g in sched]
         assert sched == sorted(sched, key=lad.index), P   # ladder order
         for i in range(len(lad) - 1):                      # each gadget on its fewest rounds
             c = sched.index(lad[i + 1])
@@ -138,17 +138,27 @@ def test_mid_gadget_plan():
                 fewer = sched[:c - 1] + [lad[i + 1]] * (len(sched) - c + 1)
                 assert _sched_worst(p, d, fewer) < 9.2, (P, i)
         nomid = replace(p, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid2_base_log=0, pbs_mid2_level=0,
-                        pbs_mid_group=0, pbs_mid2_group=0)
+                        pbs_mid_group=0, pbs_mid2_group=0, pbs_mid0_base_log=0, pbs_mid0_level=0,
+                        pbs_mid0_group=0)
         assert plan_cost(p) < plan_cost(nomid), P
-        classic = replace(p, pbs_mid_group=0, pbs_mid2_group=0)
+        classic = replace(p, pbs_mid_group=0, pbs_mid2_group=0, pbs_mid0_group=0)
         assert plan_cost(p) < plan_cost(classic), P
-    # C5's width: 1 main (6,7) classic ((5,8) before the multi-bit rounds'
-    # single rounding per pair), 2 mid (8,5) and 2 mid2 (12,3) multi-bit,
-    # 4 fast, 4 fast2
+    # C5's width: the first round on the mid0 gadget, multi-bit (5,8) (the
+    # classic main (6,7) key is made, never launched; 2.6 % cheaper than
+    # that round on it), 2 mid (8,5) and 2 mid2 (12,3) multi-bit, 4 fast,
+    # 4 fast2; P = 25 the same with a (6,7) mid0
     p26 = params_for_bits(26)
     assert (p26.pbs_base_log, p26.pbs_level, p26.pbs_mid_base_log, p26.pbs_mid_level,
             p26.pbs_mid2_base_log, p26.pbs_mid2_level) == (6, 7, 8, 5, 12, 3)
-    assert sign_schedule(p26)[1] == [0, 3, 3, 4, 4] + [1] * 4 + [2] * 4
+    assert (p26.pbs_mid0_base_log, p26.pbs_mid0_level, p26.pbs_mid0_group) == (5, 8, 2)
+    assert sign_schedule(p26)[1] == [5, 3, 3, 4, 4] + [1] * 4 + [2] * 4
+    assert plan_cost(p26) < 0.975 * plan_cost(replace(p26, pbs_mid0_base_log=0, pbs_mid0_level=0,
+                                                      pbs_mid0_group=0))
+    p25 = params_for_bits(25)
+    assert (p25.pbs_mid0_base_log, p25.pbs_mid0_level, p25.pbs_mid0_group) == (6, 7, 2)
+    assert sign_schedule(p25)[1][0] == 5
+    # mid0 is added only where it makes the plan cheaper: no width below 25
+    assert not any(params_for_bits(P).pbs_mid0_level for P in range(2, 25))
     # the headline width runs every round on the multi-bit fast gadgets: the
     # main (15, 2) key is made but never launched
     assert sign_schedule(params_for_bits(16))[1] == [1, 1, 1, 2, 2, 2, 2]
