@@ -282,30 +282,51 @@ def pipelined(batch: int) -> bool:
 GADGET_ID = {"main": 0, "fast": 1, "fast2": 2, "mid": 3, "mid2": 4, "mid0": 5}
 
 
-def isolated_br(eng, brs, reps: int = 3) -> dict:
+def pipe_split(count: int):
+    """The two halves fhe_compare_batch's pipelined sign extraction launches
+    (fheicp.hip sign_extract_batch: the first a whole number of
+    1024-ciphertext waves nearest count / 2)."""
+    if count < 2048:
+        c0 = ((count // 2) + 3) & ~3
+    else:
+        c0 = min(max(1024, 1024 * ((count + 1024) // 2048)), count - 4)
+    return c0, count - c0
+
+
+def isolated_br(eng, brs, batch: int, reps: int = 3) -> dict:
     """Per-kernel launch times without the pipelined step's overlap: every
     blind-rotation kernel the step launched, run alone (fhe_pbs_gadget_batch,
-    one stream) at the step's ciphertexts per launch on fresh key-switched
-    inputs, HIP events around each launch (after the timed region)."""
+    one stream) at the step's two half-batch sizes (pipe_split) on fresh
+    key-switched inputs, HIP events around each launch (after the timed
+    region); the totals cover both halves, so avg_launch_ms and
+    cts_per_launch are those of the step's launches."""
     out = {}
+    halves = pipe_split(batch)
     for g, b in brs.items():
         if not b["launches"]:
             continue
-        cts = int(round(b["items"] / b["launches"]))
-        v = np.where(np.arange(cts) % 2 == 0, 1, -1).astype(np.int64) << 10
-        small = eng.keyswitch(eng.encrypt(v, seed=99), 0, 0)
-        eng.pbs_gadget(small, GADGET_ID[g], 1 << 61)        # warm-up
-        torch.cuda.synchronize()
-        eng.profile(True)
-        for _ in range(reps):
-            eng.pbs_gadget(small, GADGET_ID[g], 1 << 61)
-        torch.cuda.synchronize()
-        eng.profile(False)
-        r = eng.profile_read(f"blind_rotate_{g}")
-        r["kernel"] = eng.kernel_name(f"blind_rotate_{g}")
-        assert r["kernel"] == b["kernel"], (r["kernel"], b["kernel"])
-        out[g] = r
-        del small
+        tot = None
+        for cts in halves:
+            v = np.where(np.arange(cts) % 2 == 0, 1, -1).astype(np.int64) << 10
+            small = eng.keyswitch(eng.encrypt(v, seed=99), 0, 0)
+            eng.pbs_gadget(small, GADGET_ID[g], 1 << 61)        # warm-up
+            torch.cuda.synchronize()
+            eng.profile(True)
+            for _ in range(reps):
+                eng.pbs_gadget(small, GADGET_ID[g], 1 << 61)
+            torch.cuda.synchronize()
+            eng.profile(False)
+            r = eng.profile_read(f"blind_rotate_{g}")
+            r["kernel"] = eng.kernel_name(f"blind_rotate_{g}")
+            assert r["kernel"] == b["kernel"], (r["kernel"], b["kernel"])
+            if tot is None:
+                tot = r
+            else:
+                for key in ("launches", "items", "total_ms"):
+                    tot[key] += r[key]
+            del small
+        tot["halves"] = list(halves)
+        out[g] = tot
     return out
 
 
@@ -355,7 +376,8 @@ def roofline(p, brs, batch: int = 0, iso: dict | None = None) -> dict:
         # per-launch times include the other half's kernel: `achieved` then
         # uses the same kernel's isolated launches at the same batch
         "overlapped_launches": pipelined(batch) and not iso,
-        "time_source": ("isolated launches at the step's batch after the timed region (pipelined step)"
+        "time_source": ("isolated launches at the step's two half-batch sizes after the timed region "
+                        "(pipelined step)"
                         if iso else "HIP events on the step's launches"),
         "flops_source": k["flops_source"],
         "avg_launch_ms": k["avg_launch_ms"],
@@ -441,7 +463,7 @@ def main():
     value = compares / elapsed
     ms_step = elapsed / args.steps * 1e3
 
-    roof = roofline(p, br, B, isolated_br(eng, br) if pipelined(B) else None)
+    roof = roofline(p, br, B, isolated_br(eng, br, B) if pipelined(B) else None)
     # every rank checks its own shard against the clear restatement of the
     # reference path; the flags meet in one all-reduce (MIN)
     par = shard_parity(args, model, q_np, docs_np, acc, below, T)

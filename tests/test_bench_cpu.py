@@ -142,3 +142,18 @@ def test_bare_single_rank_has_no_group():
     assert not torch.distributed.is_initialized()
     oa, oi = sharded_topk(torch.tensor([1, 5]), None, 1, 0, host_topk, 1)
     assert oa.tolist() == [5] and oi.tolist() == [1]
+
+
+def test_pipe_split_matches_the_library_halves():
+    """bench.pipe_split mirrors fheicp.hip sign_extract_batch's halves: the
+    first a whole number of 1024-ciphertext waves nearest count / 2 (from 2048
+    ciphertexts), so the isolated launches time the step's real sizes."""
+    import bench
+    assert bench.pipe_split(12500) == (6144, 6356)
+    assert bench.pipe_split(10000) == (5120, 4880)
+    assert bench.pipe_split(2048) == (1024, 1024)
+    assert bench.pipe_split(2050) == (1024, 1026)
+    assert bench.pipe_split(1000) == (500, 500)
+    for n in (2048, 3000, 4095, 4096, 12500, 100000):
+        c0, c1 = bench.pipe_split(n)
+        assert c0 % 1024 == 0 and c0 + c1 == n and c1 >= 4 and abs(c0 - n / 2) <= 512
