@@ -66,7 +66,7 @@ struct fhe_ctx {
   ProfAcc prof_br, prof_brf[5], prof_ks;  // blind rotation on the main / fast / fast2 / mid / mid2 / mid0 gadget
   ProfAcc prof_enc;                       // the fused client encryption + leveled dot (k_encrypt_linear)
   int br_variant = 4;  // N=1024 blind rotation: 4 = a wave per GLWE component (k = 2, default), 2
-                       // (two waves per ciphertext; forced by FHEICP_BR_VARIANT=2), 3 (A/B builds)
+                       // (two waves per ciphertext; forced by FHEICP_BR_VARIANT=2)
   // A/B builds only (FHEICP_AB, tools/build_variant.sh): other v4 shapes
   int v4_g = 4;        // v4 ciphertexts per workgroup (FHEICP_V4_G = 1, 2 or 4)
   int v4_fl = 0;       // v4 per-ciphertext LDS hand-offs instead of s_barrier (FHEICP_V4_FL=1)
@@ -401,9 +401,6 @@ int fhe_ctx_create(const fhe_params* params, int device, fhe_ctx** out) {
   if (const char* e = getenv("FHEICP_BR_VARIANT")) {
     const int v = atoi(e);
     ctx->br_variant = (v == 2 || v == 4) ? v : 4;
-#ifdef FHEICP_AB
-    if (v == 3) ctx->br_variant = 3;
-#endif
   }
 #ifdef FHEICP_AB
   if (const char* e = getenv("FHEICP_V4_DBG")) ctx->v4_dbg = atoi(e);
@@ -638,10 +635,6 @@ static void bsk_to_fft(fhe_ctx* ctx, const fhe_params& p, const u64* bsk, c64* b
       if (variant_for(ctx, p) == 4 || words)
         hipLaunchKernelGGL(k_bsk_to_fft_v4, dim3(std::min(npoly, 4096)), dim3(64), 0, st, bsk, npoly, ctx->tw4,
                            bsk_fft, 1.0 / 18446744073709551616.0 / (double)(p.N / 2), words && mb_xpose(p.pbs_level) ? 1 : 0);
-#ifdef FHEICP_AB
-      else if (variant_for(ctx, p) == 3)
-        hipLaunchKernelGGL(k_bsk_to_fft_mw<V3>, dim3(npoly), dim3(V3::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
-#endif
       else
         hipLaunchKernelGGL(k_bsk_to_fft_mw<V2>, dim3(npoly), dim3(V2::NT), 0, st, bsk, npoly, ctx->tw, ctx->twist, bsk_fft);
       break;
@@ -1138,10 +1131,6 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
 #ifdef FHEICP_AB
   if (p.N == 1024 && p.k == 2 && var == 4) done = launch_br_ab(ctx, p, d_small, count, tv, mode, out, ct_v, refreshed, sign,
                                                                bsk_fft, st, &name);
-  if (p.N == 1024 && var == 3) {
-    if (p.k == 1) BRV(V3, 1, 4); else BRV(V3, 2, 4);
-    done = true;
-  }
 #endif
   if (done) {
   } else if (fast && mb_for(ctx->p, gad)) {

@@ -1,5 +1,4 @@
-// Blind rotation kernels: v1 (one wave), v2 (br_m512.h), v4 (br_v4.h, the default);
-// v3 (br_m512q.h) only in A/B builds (FHEICP_AB, tools/build_variant.sh).
+// Blind rotation kernels: v1 (one wave), v2 (br_m512.h), v4 (br_v4.h, the default).
 // Part of libfheicp (one translation unit: fheicp.hip includes it).
 #pragma once
 
@@ -7,9 +6,6 @@
 
 #include "common.h"
 #include "br_m512.h"
-#ifdef FHEICP_AB
-#include "br_m512q.h"
-#endif
 #include "br_v4.h"
 
 template <int LOGM, int K, class TV = BrTv>
@@ -107,8 +103,7 @@ __global__ void __launch_bounds__(64) k_blind_rotate(const u64* __restrict__ sma
 // IEEE division and rint make this bit-identical to numpy.
 
 // ---- blind rotation for N = 1024, several waves per ciphertext -------------
-// V = V2 (br_m512.h: 2 waves, 4 complex/lane) or V3 (br_m512q.h: 4 waves,
-// 2 complex/lane); both share this kernel body.
+// V = V2 (br_m512.h: 2 waves, 4 complex/lane).
 // BSK conversion for v2: one 128-thread workgroup per polynomial, same FFT
 // as the blind rotation, stored at [u][tid] (LCs layout) and scaled by 1/M.
 template <class V>
