@@ -1,5 +1,5 @@
 #!/bin/bash
-# The bench lines of tools/closing_r03.sh alone (C2, C3, C4 shard, C5, embed),
+# The bench lines of tools/closing_r05.sh alone (C2, C3, C4 shard, C5, embed),
 # for a rerun on another box with the committed profiles/br_pmc.json of this
 # build: tools/bench_lines.sh TAG -> gpurun_out/TAG_*.json
 set -u -o pipefail
