@@ -226,8 +226,8 @@ int fhe_sign_pbs_count(const fhe_params* params);
  * without a fast gadget */
 int fhe_sign_precise_rounds(const fhe_params* params);
 /* the whole plan: digit width, bootstraps [0, main_rounds) on the main
- * gadget, [main_rounds, fast_end) on the mid, mid2 and fast ones (in that
- * order, fhe_sign_schedule), the rest on fast2
+ * gadget, [main_rounds, fast_end) on the mid0, mid, mid2 and fast ones (in
+ * that order, fhe_sign_schedule), the rest on fast2
  * (DESIGN.md §3.6). Any pointer may be NULL. */
 int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_rounds, int32_t* fast_end);
 /* the gadget (0..5, as fhe_pbs_gadget_batch) of every bootstrap of

@@ -238,8 +238,8 @@ class RefTFHE:
         return out
 
     def pbs_gadget(self, small: np.ndarray, gadget: int, tv: int) -> np.ndarray:
-        """pbs_const on gadget 0 (main), 1 (fast), 2 (fast2), 3 (mid) or 4
-        (mid2), classic or multi-bit by that gadget's group
+        """pbs_const on gadget 0 (main), 1 (fast), 2 (fast2), 3 (mid), 4
+        (mid2) or 5 (mid0), classic or multi-bit by that gadget's group
         (fhe_pbs_gadget_batch)."""
         small = np.ascontiguousarray(small, dtype=np.uint64)
         cnt = small.size // (self.n + 1)
