@@ -380,10 +380,12 @@ def test_sign_toy_three_gadgets_vs_oracle(need_gpu, oracle_lib, P, dbits):
 
 
 @pytest.mark.parametrize("P,dbits,fast", [(16, 0, True), (16, 3, True), (16, 0, "classic"), (19, 0, True),
-                                          (19, 0, False), (21, 0, True), (21, 0, False), (26, 0, True)])
+                                          (19, 0, False), (21, 0, True), (21, 0, False), (25, 0, True),
+                                          (26, 0, True)])
 def test_sign_real_params(need_gpu, P, dbits, fast):
     """Real parameters at the C2/C4 (P=16: 4-bit digits, and 3-bit forced),
-    C3 (P=21: 3-bit) and C5 (P=26: five gadgets with the mid ones) widths,
+    C3 (P=21: 3-bit) and C5 (P=26: six gadgets, the first round on the
+    multi-bit mid0 (5,8); P=25: mid0 (6,7)) widths,
     with (fast; multi-bit fast gadgets) and
     without the per-round fast gadgets, and with the fast gadgets on the
     classic rotation ("classic"), boundaries included."""
