@@ -272,7 +272,8 @@ def _br_kernel(q, br, pmc, group: int = 1) -> dict:
 
 # fhe_compare_batch splits batches of >= 2048 ciphertexts into two halves on
 # two streams (fheicp.hip PIPE_MIN, FHEICP_PIPE=0 turns it off)
-PIPE_MIN = int(os.environ.get("FHEICP_PIPE_MIN", "2048"))
+# (the library clamps an override to >= 8: sign_extract_batch)
+PIPE_MIN = max(8, int(os.environ.get("FHEICP_PIPE_MIN", "2048")))
 
 
 def pipelined(batch: int) -> bool:

@@ -108,6 +108,11 @@ static int ilog2i(int x) {
 
 static int validate(const fhe_params* p, std::string& why) {
   if (!p) { why = "null params"; return -1; }
+  if (p->struct_size != FHE_PARAMS_SIZE) {
+    why = "fhe_params.struct_size is " + std::to_string(p->struct_size) + ", this library's fhe_params has " +
+          std::to_string(FHE_PARAMS_SIZE) + " bytes: the caller was built against another include/fhe_icp.h";
+    return -1;
+  }
   if (!(p->N == 256 || p->N == 512 || p->N == 1024 || p->N == 2048)) { why = "N must be 256/512/1024/2048"; return -1; }
   if (p->k < 1 || p->k > 2) { why = "k must be 1 or 2"; return -1; }
   if (p->N == 2048 && p->k != 1) { why = "N=2048 requires k=1"; return -1; }
@@ -1428,39 +1433,60 @@ int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_r
   return FHE_OK;
 }
 
+// Trace of a sign extraction (fhe_sign_trace_batch, measurement only): an
+// explicit gadget per round instead of sign_schedule's, a stop after the
+// first `rounds` bootstraps, and the rotation exponent of every round's input
+// (k_ms_phase) into phase[round * count + c].
+struct SignTrace {
+  const int* sched = nullptr;
+  int rounds = 0;
+  uint32_t* phase = nullptr;
+};
+
 static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_sign, uint64_t* small,
-                        hipStream_t st, int lane = 0) {
-  auto keyswitch = [&](int shift, uint64_t add) {
-    return keyswitch_lane(ctx, d_ct_v, count, shift, add, small, st, lane);
-  };
+                        hipStream_t st, int lane = 0, const SignTrace* tr = nullptr) {
   const fhe_params& p = ctx->p;
   const int P = p.msg_bits, logN = log2i(p.N);
   int rc;
+  int d = 0, sched[64];
   if (P < 4) {
-    for (int i = 0; i < P; ++i) {
-      if ((rc = keyswitch(P - 1 - i, 1ull << 62))) return rc;
-      if ((rc = launch_br(ctx, small, count, BrTv{1ull << (63 - P + i), 0, 0}, 1, nullptr, d_ct_v, nullptr,
-                          (i == P - 1) ? d_sign : nullptr, st)))
-        return rc;
-    }
-    return FHE_OK;
+    for (int r = 0; r < P; ++r) sched[r] = 0;
+  } else {
+    sign_schedule(p, &d, sched);
   }
-  int d, sched[64];
-  sign_schedule(p, &d, sched);
-  const int m = P - d;
+  if (tr && tr->sched) {
+    int dd, tmp[64];
+    const int R = P < 4 ? P : sign_schedule(p, &dd, tmp);
+    for (int r = 0; r < R; ++r) sched[r] = tr->sched[r];
+  }
   int round = 0;  // bootstraps issued so far; round r runs on gadget sched[r]
-  auto br = [&](BrTv tv, int mode, uint64_t* sign) -> int {
+  // one round: key switch of v << shift, centred by `add`, then the bootstrap
+  auto step = [&](int shift, uint64_t add, BrTv tv, int mode, uint64_t* sign) -> int {
+    if (tr && tr->rounds && round >= tr->rounds) return FHE_OK;
+    int r = keyswitch_lane(ctx, d_ct_v, count, shift, add, small, st, lane);
+    if (r) return r;
+    if (tr && tr->phase) {
+      hipLaunchKernelGGL(k_ms_phase, dim3((unsigned)count), dim3(64), 0, st, p.n, logN + 1,
+                         gadget_group(p, sched[round]), ctx->s_small, small, count,
+                         tr->phase + (size_t)round * count);
+      HIPCHK(ctx, hipGetLastError());
+    }
     return launch_br(ctx, small, count, tv, mode, nullptr, d_ct_v, nullptr, sign, st, sched[round++]);
   };
+  if (P < 4) {
+    for (int i = 0; i < P; ++i)
+      if ((rc = step(P - 1 - i, 1ull << 62, BrTv{1ull << (63 - P + i), 0, 0}, 1, (i == P - 1) ? d_sign : nullptr)))
+        return rc;
+    return FHE_OK;
+  }
+  const int m = P - d;
   // one c-bit digit at bit b: the pair of rounds on v << (P-b-c) centred by 2^(63-c)
   auto digit = [&](int b, int c) -> int {
     int r;
     // digit MSB (bit b+c-1): sign bootstrap, ct_v -= [bit] * 2^(b+c-1) * Delta
-    if ((r = keyswitch(P - b - c, 1ull << (63 - c)))) return r;
-    if ((r = br(BrTv{1ull << (62 - P + b + c), 0, 0}, 1, nullptr))) return r;
+    if ((r = step(P - b - c, 1ull << (63 - c), BrTv{1ull << (62 - P + b + c), 0, 0}, 1, nullptr))) return r;
     // bits [b, b+c-1): top bit is now 0 -> 2^(c-1)-slot staircase, output D' * 2^b * Delta
-    if ((r = keyswitch(P - b - c, 1ull << (63 - c)))) return r;
-    return br(BrTv{0, 1ull << (64 - P + b), logN - (c - 1)}, 2, nullptr);
+    return step(P - b - c, 1ull << (63 - c), BrTv{0, 1ull << (64 - P + b), logN - (c - 1)}, 2, nullptr);
   };
   int b = 0;
   for (; b + d <= m; b += d)
@@ -1469,13 +1495,10 @@ static int sign_extract(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t*
     if ((rc = digit(b, m - b))) return rc;
     b = m;
   }
-  for (; b < m; ++b) {
-    if ((rc = keyswitch(P - b - 1, 1ull << 62))) return rc;
-    if ((rc = br(BrTv{1ull << (63 - P + b), 0, 0}, 1, nullptr))) return rc;
-  }
+  for (; b < m; ++b)
+    if ((rc = step(P - b - 1, 1ull << 62, BrTv{1ull << (63 - P + b), 0, 0}, 1, nullptr))) return rc;
   // sign = MSB of the top digit [P-d, P)
-  if ((rc = keyswitch(0, 1ull << (63 - d)))) return rc;
-  return br(BrTv{1ull << 62, 0, 0}, 1, d_sign);
+  return step(0, 1ull << (63 - d), BrTv{1ull << 62, 0, 0}, 1, d_sign);
 }
 
 // The sign extraction of a large batch (>= PIPE_MIN ciphertexts) in two
@@ -1536,6 +1559,36 @@ int fhe_sign_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_si
   rc = ensure_ws(ctx, 8 * (size_t)count * fhe_small_lwe_words(&ctx->p));
   if (rc) return rc;
   return sign_extract_batch(ctx, d_ct_v, count, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream);
+}
+
+int fhe_sign_trace_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, const int32_t* h_sched, int32_t rounds,
+                         uint64_t* d_sign, uint32_t* d_phase, void* stream) {
+  int rc = need_keys(ctx);
+  if (rc) return rc;
+  const fhe_params& p = ctx->p;
+  int d, tmp[64];
+  const int R = p.msg_bits < 4 ? p.msg_bits : sign_schedule(p, &d, tmp);
+  if (count < 0 || rounds < 0 || rounds > R || (count > 0 && !d_ct_v) ||
+      (count > 0 && (rounds == 0 || rounds == R) && !d_sign))
+    return fail(ctx, FHE_E_ARG, "bad sign-trace arguments (0 <= rounds <= the plan's bootstraps; d_sign when the "
+                                "last round runs)");
+  int sched[64];
+  if (h_sched) {
+    for (int r = 0; r < R; ++r) {
+      const int g = h_sched[r];
+      if (g < 0 || g >= NGAD || (g > 0 && !fast_level(p, g)))
+        return fail(ctx, FHE_E_ARG, "sign-trace schedule names a gadget these parameters do not have");
+      sched[r] = g;
+    }
+  }
+  if (count == 0) return FHE_OK;
+  rc = ensure_ws(ctx, 8 * (size_t)count * fhe_small_lwe_words(&p));
+  if (rc) return rc;
+  SignTrace tr;
+  tr.sched = h_sched ? sched : nullptr;
+  tr.rounds = rounds;
+  tr.phase = d_phase;
+  return sign_extract(ctx, d_ct_v, count, d_sign, (uint64_t*)ctx->ws, (hipStream_t)stream, 0, &tr);
 }
 
 int fhe_bit_extract_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, uint64_t* d_refreshed, uint64_t* d_sign,

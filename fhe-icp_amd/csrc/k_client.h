@@ -496,6 +496,36 @@ __global__ void __launch_bounds__(256) k_linear_seeded(ChaKey Km, int dim, const
   }
 }
 
+// The rotation exponent a blind rotation will apply to small LWE c, i.e. its
+// phase modulus-switched to 2N exactly as the rotation rounds it (measurement
+// only: it reads the small secret key, like k_decrypt): phi = b~ - sum a~_S
+// mod 2N, the test-vector index coefficient 0 ends up reading. group 1
+// (classic): a~_i = round(a_i 2N / 2^64) for every set key bit (oracle pbs1g);
+// group 2 (multi-bit pairs): the exponent of the pair's active subset, a~_1,
+// a~_2, or the switch of the exact sum a_1 + a_2 when both bits are set
+// (oracle pbs1_mb, k_blind_rotate_mb's atab). One wave per ciphertext.
+__global__ void __launch_bounds__(64) k_ms_phase(int n, int log2n2, int group, const u64* __restrict__ s,
+                                                 const u64* __restrict__ small, int64_t count,
+                                                 uint32_t* __restrict__ out) {
+  const int64_t c = blockIdx.x;
+  if (c >= count) return;
+  const u64* x = small + (size_t)c * (n + 1);
+  uint32_t part = 0;
+  if (group == 2) {
+    for (int j = threadIdx.x; 2 * j < n; j += 64) {
+      const bool s1 = s[2 * j] != 0, s2 = 2 * j + 1 < n && s[2 * j + 1] != 0;
+      if (s1 && s2) part += modswitch_2n(x[2 * j] + x[2 * j + 1], log2n2);
+      else if (s1) part += modswitch_2n(x[2 * j], log2n2);
+      else if (s2) part += modswitch_2n(x[2 * j + 1], log2n2);
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += 64)
+      if (s[i]) part += modswitch_2n(x[i], log2n2);
+  }
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off, 64);
+  if (threadIdx.x == 0) out[c] = (modswitch_2n(x[n], log2n2) - part) & ((1u << log2n2) - 1);
+}
+
 // mode 0: decode signed msg_bits integer; 1: bit (nearer 2^63); 2: raw phase
 __global__ void __launch_bounds__(256) k_decrypt(int dim, int msg_bits, int mode, const u64* __restrict__ s,
                                                  const u64* __restrict__ ct, int64_t* __restrict__ out) {

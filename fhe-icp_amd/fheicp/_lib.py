@@ -29,7 +29,9 @@ OPTIONAL_FIELDS = PARAM_FIELDS[PARAM_FIELDS.index("sign_digit_bits"):]
 
 
 class FheParams(C.Structure):
-    _fields_ = [(f, C.c_int32) for f in PARAM_FIELDS]
+    # struct_size first (= sizeof(fhe_params), checked by the library:
+    # include/fhe_icp.h), then the scheme parameters
+    _fields_ = [("struct_size", C.c_int32)] + [(f, C.c_int32) for f in PARAM_FIELDS]
 
 
 # (name, restype, argtypes) for every symbol declared in include/fhe_icp.h
@@ -76,6 +78,7 @@ SIGNATURES = [
     ("fhe_sign_precise_rounds", C.c_int, [_P]),
     ("fhe_sign_plan", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("fhe_sign_schedule", C.c_int, [_P, C.POINTER(C.c_int32), _i32]),
+    ("fhe_sign_trace_batch", C.c_int, [_CTXP, _vp, _i64, C.POINTER(C.c_int32), _i32, _vp, _vp, _vp]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_pbs_table_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _i32, _vp, _vp]),
     ("fhe_threshold_batch", C.c_int, [_CTXP, _vp, _i64, _i64, _vp, _vp]),
@@ -155,4 +158,5 @@ def check(rc: int, ctx=None) -> None:
 
 
 def params_struct(d: dict) -> FheParams:
-    return FheParams(**{f: int(d.get(f, 0) if f in OPTIONAL_FIELDS else d[f]) for f in PARAM_FIELDS})
+    return FheParams(struct_size=C.sizeof(FheParams),
+                     **{f: int(d.get(f, 0) if f in OPTIONAL_FIELDS else d[f]) for f in PARAM_FIELDS})

@@ -249,6 +249,30 @@ class Engine:
         self._chk(self._L.fhe_sign_batch(self._ctx, _ptr(ct_v), n, _ptr(sign), _stream(self.device)))
         return sign
 
+    def sign_trace(self, ct_v: torch.Tensor, sched=None, rounds: int = 0, phases: bool = True):
+        """Measurement only (fhe_sign_trace_batch): consumes ct_v and runs the
+        sign extraction's rounds (all, or the first `rounds`) on an explicit
+        gadget schedule (None: the plan's). Returns (sign ciphertexts or None,
+        phases uint32 tensor [R][count] of every round's rotation exponent or
+        None)."""
+        n = ct_v.numel() // self.W
+        R = len(sched) if sched is not None else None
+        if R is None:
+            cap = (C.c_int32 * 64)()
+            R = self._L.fhe_sign_schedule(C.byref(self._P_now()), cap, 64)
+            if R < 0:
+                _lib.check(R)
+        last = rounds in (0, R)
+        sign = self.empty_big(n) if last else None
+        ph = torch.empty((R, n), dtype=torch.int32, device=self.device) if phases else None
+        hs = (C.c_int32 * R)(*[int(g) for g in sched]) if sched is not None else None
+        self._chk(self._L.fhe_sign_trace_batch(self._ctx, _ptr(ct_v), n, hs, int(rounds), _ptr(sign), _ptr(ph),
+                                               _stream(self.device)))
+        return sign, ph
+
+    def _P_now(self):
+        return _lib.params_struct(self.params.as_dict())
+
     def bit_extract(self, ct_v: torch.Tensor):
         """Consumes ct_v; returns (refreshed, sign) ciphertexts."""
         n = ct_v.numel() // self.W

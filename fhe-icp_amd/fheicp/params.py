@@ -119,6 +119,58 @@ def sign_rounds(P: int, d: int):
     return out
 
 
+def sign_round_ops(P: int, d: int, N: int):
+    """Every round of fhe_sign_batch as the library issues it (fheicp.hip
+    sign_extract), for measuring it: the key switch of v << shift centred by
+    `add`, the bootstrap's test vector (base, step, tv_shift) and mode, and
+    the bits of v already cleared when the round runs: the round decides on
+    v_cur = v with bits [0, lo) and the bit `hi` (if not None) cleared."""
+    logN = N.bit_length() - 1
+    ops = []
+    if P < 4:
+        for i in range(P):
+            ops.append(dict(shift=P - 1 - i, add=1 << 62, tv=(1 << (63 - P + i), 0, 0), mode=1, lo=i, hi=None))
+        return ops
+    m = P - d
+
+    def digit(b, c):
+        ops.append(dict(shift=P - b - c, add=1 << (63 - c), tv=(1 << (62 - P + b + c), 0, 0), mode=1, lo=b, hi=None))
+        ops.append(dict(shift=P - b - c, add=1 << (63 - c), tv=(0, 1 << (64 - P + b), logN - (c - 1)), mode=2,
+                        lo=b, hi=b + c - 1))
+    b = 0
+    while b + d <= m:
+        digit(b, d)
+        b += d
+    if m - b >= 3:
+        digit(b, m - b)
+        b = m
+    while b < m:
+        ops.append(dict(shift=P - b - 1, add=1 << 62, tv=(1 << (63 - P + b), 0, 0), mode=1, lo=b, hi=None))
+        b += 1
+    ops.append(dict(shift=0, add=1 << (63 - d), tv=(1 << 62, 0, 0), mode=1, lo=m, hi=None))
+    return ops
+
+
+def sign_round_sigmas(p: "SchemeParams", sched=None):
+    """The noise model of every decision of the sign extraction, round by
+    round (the terms of _sched_worst): [(shift, log2 margin, sigma)], sigma
+    relative to the torus, on the plan's schedule or an explicit one. The
+    input ciphertext's own noise is not in it (the caller adds it)."""
+    d, plan = sign_schedule(p)
+    sched = list(plan if sched is None else sched)
+    rounds = sign_rounds(p.msg_bits, d)
+    if len(sched) != len(rounds):
+        raise ValueError(f"schedule has {len(sched)} rounds, the plan {len(rounds)}")
+    vs = {g: _gadget_var(p, g) for g in set(sched)}
+    vms = {g: _ms_var(p, gadget_of(p, g)[2]) for g in set(sched)}
+    _, v_ks, _ = _variances(p)
+    acc, out = 0.0, []
+    for r, (sh, ml) in enumerate(rounds):
+        out.append((sh, ml, math.sqrt(acc * 4.0 ** sh + v_ks + vms[sched[r]])))
+        acc += vs[sched[r]]
+    return out
+
+
 # gadget ids (fhe_pbs_gadget_batch): 0 main, 1 fast, 2 fast2, 3 mid, 4 mid2, 5 mid0
 GADGET_IDS = (0, 1, 2, 3, 4, 5)
 

@@ -22,14 +22,20 @@ def sharded_topk(acc: torch.Tensor, below: torch.Tensor | None, k: int, base_idx
 
     Returns the global top-k (identical on every rank). The exchange runs
     whenever a process group exists, a one-rank group included (so a
-    one-GPU launcher run executes the RCCL all-gather too); without one,
-    world must be 1."""
+    one-GPU launcher run executes the RCCL all-gather too), and world must
+    then equal the group's size (ValueError otherwise); without one, world
+    must be 1."""
     oa, oi = topk_fn(acc, below, k, base_idx)
     if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
         if world != 1:
             raise RuntimeError(f"sharded_topk: world {world} without a process group")
         return oa, oi
-    world = torch.distributed.get_world_size(group)
+    if world != torch.distributed.get_world_size(group):
+        # a caller meaning a local (replicated) search inside a multi-rank job
+        # would otherwise merge every rank's duplicates, or hang when the
+        # other ranks do not join: refuse instead of overriding the argument
+        raise ValueError(f"sharded_topk: world {world} but the process group has "
+                         f"{torch.distributed.get_world_size(group)} ranks")
     # one collective: the k (acc, index) pairs travel packed as [k, 2] int64.
     # RCCL gathers device tensors in place; other backends (gloo rehearsals)
     # go through host copies

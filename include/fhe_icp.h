@@ -43,8 +43,14 @@ extern "C" {
 #define FHE_E_STATE (-3)    /* keys not generated / imported */
 #define FHE_E_NOMEM (-4)
 
-/* Scheme parameters. Same field order as the oracle's. */
+/* Scheme parameters. After struct_size, the oracle's field
+ * order (oracle/tfhe_ref.c ref_params). */
 typedef struct fhe_params {
+  int32_t struct_size;     /* = sizeof(fhe_params) (FHE_PARAMS_SIZE): every entry point
+                              that reads a fhe_params checks it, so a binding built
+                              against another version of this header (fewer or more
+                              fields) fails with FHE_E_ARG instead of reading past
+                              its struct or misreading fields */
   int32_t n;               /* small LWE dimension (blind-rotation length) */
   int32_t k;               /* GLWE dimension (1 or 2) */
   int32_t N;               /* polynomial size: 256, 512, 1024 or 2048 */
@@ -91,6 +97,7 @@ typedef struct fhe_params {
                                 multi-bit). Key: fhe_export_fast_bsk
                                 which = 5 (stream tags 25/26, 27/28 multi-bit). */
 } fhe_params;
+#define FHE_PARAMS_SIZE ((int32_t)sizeof(fhe_params))
 
 typedef struct fhe_ctx fhe_ctx;
 
@@ -234,6 +241,20 @@ int fhe_sign_plan(const fhe_params* params, int32_t* digit_bits, int32_t* main_r
  * fhe_sign_batch in order, into gadgets[0 .. min(R, cap)); returns R (the
  * bootstraps per sign extraction) or FHE_E_ARG on bad params. */
 int fhe_sign_schedule(const fhe_params* params, int32_t* gadgets, int32_t cap);
+/* MEASUREMENT ONLY (reads the secret key; no reference counterpart): the
+ * decision noise behind the exactness of fhe_sign_batch (the decision of
+ * batch_operations.py:278). Runs fhe_sign_batch's rounds on one stream, with
+ *  - h_sched (host, R entries, NULL = fhe_sign_schedule's plan): the gadget
+ *    of every round, e.g. a deliberately noisier one to narrow a margin;
+ *  - rounds: stop after the first `rounds` bootstraps (0 = all R); d_sign is
+ *    written (and required) only when the last round runs;
+ *  - d_phase (device, NULL = none): round r's rotation exponent for
+ *    ciphertext c at d_phase[r * count + c], the bootstrap input's phase
+ *    modulus-switched to 2N exactly as that round's rotation (classic or
+ *    multi-bit) rounds it, i.e. the test-vector index the rotation selects.
+ * tests/test_gpu_decision_noise.py compares these with the exact rounds. */
+int fhe_sign_trace_batch(fhe_ctx* ctx, uint64_t* d_ct_v, int64_t count, const int32_t* h_sched, int32_t rounds,
+                         uint64_t* d_sign, uint32_t* d_phase, void* stream);
 /* Bootstrap with a staircase test vector over 2^log_slots slots of the half
  * torus: output phase ~ base + floor(phase * 2^log_slots / 2^63) * step for an
  * input phase in [0, 2^63) (negacyclic beyond). log_slots = 0, step = 0 is

@@ -30,7 +30,8 @@ FIELDS = ("n", "k", "N", "pbs_base_log", "pbs_level", "ks_base_log", "ks_level",
 
 
 class fhe_params(C.Structure):
-    _fields_ = [(f, C.c_int32) for f in FIELDS]
+    # struct_size (= sizeof(fhe_params), checked by the library) leads
+    _fields_ = [("struct_size", C.c_int32)] + [(f, C.c_int32) for f in FIELDS]
 
 
 _vp, _i32, _i64, _u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
@@ -67,7 +68,7 @@ class GpuCompare:
         for name, (res, args) in _PROTOS.items():
             getattr(L, name).restype = res
             getattr(L, name).argtypes = args
-        self.P = fhe_params(**{f: int(params.get(f, 0)) for f in FIELDS})
+        self.P = fhe_params(struct_size=C.sizeof(fhe_params), **{f: int(params.get(f, 0)) for f in FIELDS})
         self.ctx = _vp()
         self._ok(L.fhe_ctx_create(C.byref(self.P), device, C.byref(self.ctx)))
         if key_seed is None:

@@ -1122,7 +1122,8 @@ void ref_sign_extract_keys(const ref_params* P0, const uint64_t* bsk, const uint
 }
 void ref_sign_extract3(const ref_params* P, const uint64_t* bsk, const uint64_t* bsk2, const uint64_t* bsk3,
                        const uint64_t* ksk, uint64_t* ct_v, int64_t count, uint64_t* sign) {
-  const uint64_t* keys[4] = {bsk2, bsk3, NULL, NULL};
+  /* one slot per gadget 1 .. NGAD - 1 (ref_sign_extract_keys reads them all) */
+  const uint64_t* keys[NGAD - 1] = {bsk2, bsk3, NULL, NULL, NULL};
   ref_sign_extract_keys(P, bsk, keys, ksk, ct_v, count, sign);
 }
 void ref_sign_extract(const ref_params* P, const uint64_t* bsk, const uint64_t* ksk, uint64_t* ct_v, int64_t count,

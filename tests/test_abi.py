@@ -285,3 +285,33 @@ def test_gemm_lds_dma_pipelines_not_drained():
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     assert r.stdout.count("k_gemm") >= 6
+
+
+def test_params_struct_size_refuses_stale_bindings():
+    """fhe_params leads with struct_size, checked by every entry
+    point that validates parameters. A binding built against the previous
+    header (no struct_size, 26 fields) puts n = 887 in its place and is
+    refused with FHE_E_ARG instead of read past its end; the Python binding's
+    field list is the header's."""
+    import re
+    hdr = (Path(__file__).resolve().parents[1] / "include" / "fhe_icp.h").read_text()
+    body = re.search(r"typedef struct fhe_params \{(.*?)\} fhe_params;", hdr, re.S).group(1)
+    fields = re.findall(r"int32_t\s+(\w+);", body)
+    assert fields == ["struct_size"] + list(_lib.PARAM_FIELDS)
+    L = _lib.lib()
+    assert C.sizeof(_lib.FheParams) == 4 * len(fields)
+
+    class Old(C.Structure):
+        _fields_ = [(f, C.c_int32) for f in _lib.PARAM_FIELDS]
+    d = params_for_bits(16).as_dict()
+    old = Old(**{f: int(d.get(f, 0)) for f in _lib.PARAM_FIELDS})
+    h = C.c_void_p()
+    assert L.fhe_ctx_create(C.cast(C.byref(old), C.POINTER(_lib.FheParams)), -1, C.byref(h)) == -1
+    assert b"struct_size" in L.fhe_last_error(None)
+    assert L.fhe_sign_pbs_count(C.cast(C.byref(old), C.POINTER(_lib.FheParams))) == -1
+    P = _lib.params_struct(d)
+    assert P.struct_size == C.sizeof(_lib.FheParams)
+    assert L.fhe_ctx_create(C.byref(P), -1, C.byref(h)) == 0
+    got = _lib.FheParams()
+    assert L.fhe_get_params(h, C.byref(got)) == 0 and got.struct_size == P.struct_size
+    L.fhe_ctx_destroy(h)

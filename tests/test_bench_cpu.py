@@ -119,6 +119,12 @@ orig = torch.distributed.all_gather
 torch.distributed.all_gather = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
 oa, oi = sharded_topk(torch.tensor([3, 8, 8, 1]), None, 2, 10, host_topk, 1)
 assert calls == [1] and oa.tolist() == [8, 8] and oi.tolist() == [11, 12], (calls, oa, oi)
+# a world that is not the group's is refused, not silently replaced
+try:
+    sharded_topk(torch.tensor([3, 8]), None, 1, 0, host_topk, 2)
+    raise SystemExit("world 2 in a 1-rank group was accepted")
+except ValueError:
+    pass
 torch.distributed.destroy_process_group()
 open(os.path.join(sys.argv[3], "ok"), "w").close()
 """
@@ -157,3 +163,19 @@ def test_pipe_split_matches_the_library_halves():
     for n in (2048, 3000, 4095, 4096, 12500, 100000):
         c0, c1 = bench.pipe_split(n)
         assert c0 % 1024 == 0 and c0 + c1 == n and c1 >= 4 and abs(c0 - n / 2) <= 512
+
+
+def test_pipe_min_override_is_clamped_like_the_library(monkeypatch):
+    """FHEICP_PIPE_MIN below 8 is clamped to 8 in bench.py as in
+    fheicp.hip sign_extract_batch, so pipelined() / pipe_split() describe
+    the launches the library makes."""
+    import importlib
+    sys.path.insert(0, str(REPO))
+    import bench
+    monkeypatch.setenv("FHEICP_PIPE_MIN", "4")
+    b = importlib.reload(bench)
+    try:
+        assert b.PIPE_MIN == 8 and not b.pipelined(6) and b.pipelined(8)
+    finally:
+        monkeypatch.delenv("FHEICP_PIPE_MIN")
+        importlib.reload(bench)

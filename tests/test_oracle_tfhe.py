@@ -391,3 +391,25 @@ def test_keyswitch_digits_zero_mean(oracle_lib, beta, lvl):
         assert got % 2 ** 64 == want % 2 ** 64
     assert abs(ds.mean()) < 0.02
     assert abs((ds.astype(float) ** 2).mean() / ((B * B + 2) / 12) - 1) < 0.02
+
+
+def test_oracle_sign_entry_points_under_sanitizers(tmp_path):
+    """ref_sign_extract / ref_sign_extract3 pass short key arrays
+    to ref_sign_extract_keys, which reads one slot per gadget (NGAD - 1). The
+    oracle source and oracle/asan_driver.c are compiled together under
+    -fsanitize=address,undefined (gcc, no OpenMP) and both entry points run on
+    the TOY set: exact sign bits and no sanitizer report."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    ora = Path(__file__).resolve().parents[1] / "oracle"
+    exe = tmp_path / "drv"
+    subprocess.run(["gcc", "-O2", "-g", "-std=c11", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-fno-sanitize-recover=all", "-Wno-unknown-pragmas", "-o", str(exe),
+                    str(ora / "asan_driver.c"), str(ora / "tfhe_ref.c"), "-lm"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 wrong sign bits" in r.stdout
+    assert "Sanitizer" not in r.stderr, r.stderr

@@ -407,3 +407,46 @@ def test_two_word_torus_rounding_equals_split():
     hu = np.where(hi >= 2.0 ** 31, hi - 2.0 ** 32, hi).astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)
     old = (hu << np.uint64(32)) + lo.astype(np.uint64)
     assert np.array_equal(new, old)
+
+
+@pytest.mark.parametrize("P", [3, 5, 11, 15, 16, 21, 26])
+def test_sign_round_ops_clear_simulation(P):
+    """fheicp.params.sign_round_ops (the bookkeeping the decision-noise GPU
+    test measures against) run in the clear on exact phases: every round's
+    exact exponent is the centre of its slot on the 2N grid, the test vector
+    read there clears exactly the bits the next round assumes cleared, and the
+    last round's output is [v < 0]; the shifts and margins are sign_rounds'."""
+    import sys
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parent))
+    import decision_noise_lib as DL
+    from fheicp.params import sign_round_ops
+    p = params_for_bits(P)
+    d = sign_digit_bits(p)
+    N = p.N
+    ops = sign_round_ops(P, d, N)
+    if P >= 4:
+        assert [(o["shift"]) for o in ops] == [sh for sh, _ in sign_rounds(P, d)]
+    assert len(ops) == sign_pbs_count(p)
+    rng = np.random.default_rng(P)
+    v = np.arange(-(1 << (P - 1)), 1 << (P - 1), dtype=np.int64) if P <= 16 else \
+        rng.integers(-(1 << (P - 1)), 1 << (P - 1), 200000)
+    delta = np.uint64(1 << (64 - P))
+    M = v.view(np.uint64) * delta
+    sign = None
+    for r, op in enumerate(ops):
+        with np.errstate(over="ignore"):
+            assert np.array_equal(M, DL.v_cur(v, op).view(np.uint64) * delta), r
+        ideal = DL.ideal_index(v, op, P, N)
+        x = DL.tv_decode(ideal, op, N)
+        base = np.uint64(op["tv"][0])
+        with np.errstate(over="ignore"):
+            dlt = base - x if op["mode"] == 1 else x
+            M = M - dlt
+        if r == len(ops) - 1:
+            sign = dlt
+        # the margin: the nearest slot boundary is 2^(ml) of the torus away
+        if P >= 4:
+            ml = sign_rounds(P, d)[r][1]
+            d_lo, d_hi = DL.boundary_distances(op, N)
+            assert min(d_lo[ideal].min(), d_hi[ideal].min()) == (2 * N) >> (-ml)
+    assert np.array_equal(sign >> np.uint64(63), (v < 0).astype(np.uint64))
