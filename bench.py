@@ -513,6 +513,12 @@ def main():
     out["leveled_score"] = leveled_score(args, model, q_dev, d_dev, acc)
     if dist_on():
         out["allgather_ms"] = round(allgather_ms, 4)
+        out["allgather_note"] = (
+            "one all-gather of k (acc, index) pairs per rank, timed after the timed region; "
+            + ("at world size 1 it is a local copy on the device, not an xGMI transfer" if world == 1 else
+               f"{world} ranks' {args.top_k} x 16 B over "
+               + ("RCCL (xGMI between GPUs)" if torch.distributed.get_backend() == "nccl" else
+                  f"{torch.distributed.get_backend()} (host copies)")))
         out["dist"] = dist_info(dev)
     if world == 1:
         out["pcie_inclusive"] = pcie_inclusive(args, model, q_dev, docs_np, T, dev)

@@ -364,32 +364,49 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
     const u64 id = id0 + (u64)b * G + g;
     const int Dg = min(D - g * N, N);
     __syncthreads();  // the previous chunk's readers are done
-    for (int blk = threadIdx.x; blk < k * N / 8; blk += 256) {
-      u64 m[8];
-      stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) shm[8 * blk + q] = m[q];
-    }
-    EL_STAMP(2, __builtin_amdgcn_s_memtime());
     // the features' noise words, 8 per block, each block on a quad of lanes
     // (chacha20_block_quad): noise block nb on quad nb / 4 of wave nb mod 4;
     // the even lanes of the quad hold the low words of u64 words
     // j = (q + 4 r) / 2, the odd ones the high words
-    {
-      const int q = (int)(threadIdx.x & 3), wv = (int)(threadIdx.x >> 6), qd = (int)((threadIdx.x & 63) >> 2);
-      for (int nb = 4 * qd + wv; 8 * nb < Dg; nb += 64) {
-        uint32_t e4[4];
-        chacha20_block_quad(K, (uint32_t)nb, TAG_ENC_NOISE, id, q, e4);
+    const int q = (int)(threadIdx.x & 3), wv = (int)(threadIdx.x >> 6), qd = (int)((threadIdx.x & 63) >> 2);
+    auto noise_words = [&](int nb, const uint32_t e4[4]) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t hi = quad_mov<QP_XOR1>(e4[r]);
-          const int t = 8 * nb + ((q + 4 * r) >> 1);
-          if ((q & 1) == 0 && t < Dg) {
-            const u64 e = (u64)e4[r] | ((u64)hi << 32);
-            bpart += (u64)w[g * N + t] * (((u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits)) + (u64)tuniform(e, noise_bits));
-          }
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t hi = quad_mov<QP_XOR1>(e4[r]);
+        const int t = 8 * nb + ((q + 4 * r) >> 1);
+        if ((q & 1) == 0 && t < Dg) {
+          const u64 e = (u64)e4[r] | ((u64)hi << 32);
+          bpart += (u64)w[g * N + t] * (((u64)x[(size_t)b * D + g * N + t] << (64 - msg_bits)) + (u64)tuniform(e, noise_bits));
         }
       }
+    };
+    const int nblk = k * N / 8;
+    int blk = threadIdx.x, nb = 4 * qd + wv;
+    // a wave whose first quad has a noise block and whose lanes all have a
+    // mask block computes the quad blocks of its first noise pass inside its
+    // mask blocks (chacha20_block_with_quad): at D = 16 the two noise blocks
+    // ran as their own latency-bound pass on waves 0-1 (9.5k of a wave's 33k
+    // cycles) while the other waves waited at the barrier (docs/AB_LOG_r06.md)
+    if ((wv + 1) * 64 <= nblk && 8 * wv < Dg) {
+      uint32_t o[16], e4[4];
+      chacha20_block_with_quad(K, (uint32_t)blk, TAG_ENC_MASK, id, o, (uint32_t)nb, TAG_ENC_NOISE, id, q, e4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) shm[8 * blk + j] = (u64)o[2 * j] | ((u64)o[2 * j + 1] << 32);
+      if (8 * nb < Dg) noise_words(nb, e4);
+      blk += 256;
+      nb += 64;
+    }
+    for (; blk < nblk; blk += 256) {
+      u64 m[8];
+      stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) shm[8 * blk + j] = m[j];
+    }
+    EL_STAMP(2, __builtin_amdgcn_s_memtime());
+    for (; 8 * nb < Dg; nb += 64) {
+      uint32_t e4[4];
+      chacha20_block_quad(K, (uint32_t)nb, TAG_ENC_NOISE, id, q, e4);
+      noise_words(nb, e4);
     }
     EL_STAMP(3, __builtin_amdgcn_s_memtime());
     __syncthreads();

@@ -91,23 +91,84 @@ constexpr int QP_ROT1 = 0x39, QP_ROT2 = 0x4e, QP_ROT3 = 0x93, QP_XOR1 = 0xb1;  /
   c += d; b ^= c; b = rotl32(b, 12);              \
   a += b; d ^= a; d = rotl32(d, 8);               \
   c += d; b ^= c; b = rotl32(b, 7);
+// v_q of four values without an indexable array: a select chain on struct
+// words (K.w[0..3]) folded into a per-lane dynamic index made hipcc keep the
+// key in scratch (36 bytes per lane, 8.4 MB of writes per 1024-pair
+// k_encrypt_linear launch, docs/AB_LOG_r06.md); the select is two masked
+// blends, and sel4u first makes WAVE-UNIFORM words (the key, constants)
+// plain values by readfirstlane (never for per-lane or per-quad values)
+__device__ __forceinline__ uint32_t sel4(int q, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+  const uint32_t m1 = 0u - (uint32_t)(q & 1), m2 = 0u - (uint32_t)((q >> 1) & 1);
+  const uint32_t lo = v0 ^ ((v0 ^ v1) & m1), hi = v2 ^ ((v2 ^ v3) & m1);
+  return lo ^ ((lo ^ hi) & m2);
+}
+__device__ __forceinline__ uint32_t sel4u(int q, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+  return sel4(q, (uint32_t)__builtin_amdgcn_readfirstlane((int)v0), (uint32_t)__builtin_amdgcn_readfirstlane((int)v1),
+              (uint32_t)__builtin_amdgcn_readfirstlane((int)v2), (uint32_t)__builtin_amdgcn_readfirstlane((int)v3));
+}
+struct QuadState {
+  uint32_t a, b, c, d, a0, b0, c0, d0;
+};
+__device__ __forceinline__ QuadState quad_init(const ChaKey& K, uint32_t counter, uint32_t tag, uint64_t id, int q) {
+  QuadState s;
+  s.a0 = sel4(q, 0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u);
+  s.b0 = sel4u(q, K.w[0], K.w[1], K.w[2], K.w[3]);
+  s.c0 = sel4u(q, K.w[4], K.w[5], K.w[6], K.w[7]);
+  s.d0 = sel4(q, counter, tag, (uint32_t)id, (uint32_t)(id >> 32));  // counter: per quad
+  s.a = s.a0; s.b = s.b0; s.c = s.c0; s.d = s.d0;
+  return s;
+}
+// one double round of the quad block: column round, rows rotated, diagonal
+// round, rotated back
+__device__ __forceinline__ void quad_double_round(QuadState& s) {
+  FHEI_QRL(s.a, s.b, s.c, s.d)
+  s.b = quad_mov<QP_ROT1>(s.b); s.c = quad_mov<QP_ROT2>(s.c); s.d = quad_mov<QP_ROT3>(s.d);
+  FHEI_QRL(s.a, s.b, s.c, s.d)
+  s.b = quad_mov<QP_ROT3>(s.b); s.c = quad_mov<QP_ROT2>(s.c); s.d = quad_mov<QP_ROT1>(s.d);
+}
+__device__ __forceinline__ void quad_out(const QuadState& s, uint32_t out[4]) {
+  out[0] = s.a + s.a0; out[1] = s.b + s.b0; out[2] = s.c + s.c0; out[3] = s.d + s.d0;
+}
 __device__ __forceinline__ void chacha20_block_quad(const ChaKey& K, uint32_t counter, uint32_t tag, uint64_t id,
                                                     int q, uint32_t out[4]) {
-  const uint32_t a0 = q == 0 ? 0x61707865u : q == 1 ? 0x3320646eu : q == 2 ? 0x79622d32u : 0x6b206574u;
-  const uint32_t b0 = q == 0 ? K.w[0] : q == 1 ? K.w[1] : q == 2 ? K.w[2] : K.w[3];
-  const uint32_t c0 = q == 0 ? K.w[4] : q == 1 ? K.w[5] : q == 2 ? K.w[6] : K.w[7];
-  const uint32_t d0 = q == 0 ? counter : q == 1 ? tag : q == 2 ? (uint32_t)id : (uint32_t)(id >> 32);
-  uint32_t a = a0, b = b0, c = c0, d = d0;
+  QuadState s = quad_init(K, counter, tag, id, q);
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    FHEI_QRL(a, b, c, d)
-    b = quad_mov<QP_ROT1>(b); c = quad_mov<QP_ROT2>(c); d = quad_mov<QP_ROT3>(d);
-    FHEI_QRL(a, b, c, d)
-    b = quad_mov<QP_ROT3>(b); c = quad_mov<QP_ROT2>(c); d = quad_mov<QP_ROT1>(d);
-  }
-  out[0] = a + a0; out[1] = b + b0; out[2] = c + c0; out[3] = d + d0;
+  for (int r = 0; r < 10; ++r) quad_double_round(s);
+  quad_out(s, out);
 }
 #undef FHEI_QRL
+
+// A lane's own ChaCha20 block (as chacha20_block) with a quad block
+// (chacha20_block_quad) interleaved round by round: the quad's dependent
+// chain (one quarter round per lane, DPP between rounds) issues in the
+// shadow of the lane block's four independent quarter rounds instead of as a
+// latency-bound pass of its own (k_encrypt_linear's noise blocks).
+#define FHEI_QR2(a, b, c, d)                      \
+  a += b; d ^= a; d = rotl32(d, 16);              \
+  c += d; b ^= c; b = rotl32(b, 12);              \
+  a += b; d ^= a; d = rotl32(d, 8);               \
+  c += d; b ^= c; b = rotl32(b, 7);
+__device__ __forceinline__ void chacha20_block_with_quad(const ChaKey& K, uint32_t counter, uint32_t tag, uint64_t id,
+                                                         uint32_t out[16], uint32_t qcounter, uint32_t qtag,
+                                                         uint64_t qid, int q, uint32_t qout[4]) {
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = K.w[0], x5 = K.w[1], x6 = K.w[2], x7 = K.w[3];
+  uint32_t x8 = K.w[4], x9 = K.w[5], x10 = K.w[6], x11 = K.w[7];
+  uint32_t x12 = counter, x13 = tag, x14 = (uint32_t)id, x15 = (uint32_t)(id >> 32);
+  QuadState s = quad_init(K, qcounter, qtag, qid, q);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    FHEI_QR2(x0, x4, x8, x12) FHEI_QR2(x1, x5, x9, x13) FHEI_QR2(x2, x6, x10, x14) FHEI_QR2(x3, x7, x11, x15)
+    FHEI_QR2(x0, x5, x10, x15) FHEI_QR2(x1, x6, x11, x12) FHEI_QR2(x2, x7, x8, x13) FHEI_QR2(x3, x4, x9, x14)
+    quad_double_round(s);
+  }
+  out[0] = x0 + 0x61707865u; out[1] = x1 + 0x3320646eu; out[2] = x2 + 0x79622d32u; out[3] = x3 + 0x6b206574u;
+  out[4] = x4 + K.w[0]; out[5] = x5 + K.w[1]; out[6] = x6 + K.w[2]; out[7] = x7 + K.w[3];
+  out[8] = x8 + K.w[4]; out[9] = x9 + K.w[5]; out[10] = x10 + K.w[6]; out[11] = x11 + K.w[7];
+  out[12] = x12 + counter; out[13] = x13 + tag; out[14] = x14 + (uint32_t)id; out[15] = x15 + (uint32_t)(id >> 32);
+  quad_out(s, qout);
+}
+#undef FHEI_QR2
 
 // Eight consecutive u64 words [8*blk, 8*blk+8) of stream (tag, id).
 __host__ __device__ __forceinline__ void stream_block(const ChaKey& K, uint32_t tag, uint64_t id, uint32_t blk,

@@ -180,4 +180,5 @@ def test_bench_one_rank_rccl(need_gpu):
     assert par["acc_bit_exact"] and par["threshold_bit_exact"] and par["quant_params_equal"]
     assert out["topk_check"]["indices_equal"] and out["topk_check"]["scores_equal"]
     assert out["allgather_ms"] > 0
+    assert "local copy" in out["allgather_note"]   # world 1: not an xGMI number
     assert "RCCL top-k all-gather" in out["config"]["workload"]
