@@ -68,10 +68,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-compares", type=int, default=0,
                     help="oracle sample size (0: 64 compares scaled down by the sign plan's cost, 10-30 s)")
-    ap.add_argument("--mode", choices=("compare", "corpus", "embed"), default="compare",
+    ap.add_argument("--mode", choices=("compare", "corpus", "embed", "lut"), default="compare",
                     help="compare: the reference's path (configs[1]); corpus: search over a stored corpus of "
                          "seeded-LWE documents (SURVEY.md §8f-1); embed: the BERT encoder of the embedding "
-                         "stage (SURVEY.md §8f-4)")
+                         "stage (SURVEY.md §8f-4); lut: the programmable (table) bootstrap, PBS/s (SURVEY.md "
+                         "§8a row P, the north star's 'polynomial activation')")
+    ap.add_argument("--lut-bits", type=int, default=4, help="--mode lut: input message bits of the table")
+    ap.add_argument("--lut-msg-bits", type=int, default=16,
+                    help="--mode lut: output width P (the parameter set params_for_bits(P))")
     ap.add_argument("--embed-batch", type=int, default=256, help="--mode embed: sequences per forward pass")
     ap.add_argument("--seq-len", type=int, default=100, help="--mode embed: tokens per sequence (max_length)")
     ap.add_argument("--embed-precision", choices=("f32", "bf16"), default="f32",
@@ -412,6 +416,8 @@ def main():
         return corpus_main(args, world, rank, local, dev)
     if args.mode == "embed":
         return embed_main(args, world, rank, local, dev)
+    if args.mode == "lut":
+        return lut_main(args, world, rank, local, dev)
 
     model = build_model(args)
     model.compile(key_seed=args.seed, device=local)
@@ -774,6 +780,118 @@ def cpu_leg(args, model, q_np, docs_np, parity):
     t_clear = (time.perf_counter() - t0) / reps
     base["clear_path_compares_per_s"] = round(len(Xp) / t_clear, 1)
     return base
+
+
+def lut_main(args, world, rank, local, dev):
+    """--mode lut: the programmable bootstrap with an arbitrary table
+    (fhe_pbs_table_batch), the PBS a requantisation or a polynomial activation
+    of the north star would run. --docs ciphertexts of random lut_bits-bit
+    messages (one padding bit) are resident in HBM; one step = key switch +
+    table bootstrap of all of them into P-bit outputs (a random signed
+    table). The default gadget is the set's most precise multi-bit one, the
+    sign extraction's kernel family (P = 16: (15,2), k_blind_rotate_mb<2, 0,
+    15, BrTvLut>). Every output is decrypted against lut[m]; four phases
+    against the oracle's ref_pbs_table_gadget on the same keys; the sign
+    path's kernel on the same gadget and inputs is timed beside it."""
+    from dataclasses import replace
+    from fheicp.engine import Engine, u64
+    from fheicp.params import gadget_of, params_for_bits
+    P, lb, B = args.lut_msg_bits, args.lut_bits, args.docs
+    p = params_for_bits(P)
+    eng = Engine(p, local)
+    eng.keygen(args.seed)
+    gad = eng.table_gadget()
+    rng = np.random.default_rng(args.seed + 3)
+    M = 1 << lb
+    lut = rng.integers(-(2 ** (P - 1)), 2 ** (P - 1), M)
+    m = rng.integers(0, M, B)
+    eng.set_msg_bits(lb + 1)                 # the input encoding: padding bit + lut_bits
+    ct = eng.encrypt(m, seed=args.seed + 4)
+    eng.set_msg_bits(P)
+    lut_d = eng.to_dev(lut)
+    small = eng.keyswitch(ct, 0, 0)
+
+    def step():
+        sm = eng.keyswitch(ct, 0, 0)
+        return eng.pbs_table(sm, lut_d, lb)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    secs = time.perf_counter() - t0
+    eng.profile(False)
+    bucket = {0: "blind_rotate_main", 1: "blind_rotate_fast", 2: "blind_rotate_fast2", 3: "blind_rotate_mid",
+              4: "blind_rotate_mid2", 5: "blind_rotate_mid0"}[gad]
+    br = eng.profile_read(bucket)
+    br["kernel"] = eng.kernel_name(bucket)
+    ks = eng.profile_read("keyswitch")
+    bl, lv, grp = gadget_of(p, gad)
+    q = replace(p, pbs_base_log=bl, pbs_level=lv)
+    k = _br_kernel(q, br, load_pmc(), grp)
+    dec = eng.decrypt(out).cpu().numpy()
+    exact = bool(np.array_equal(dec, lut[m]))
+    # the sign extraction's kernel on the same gadget and inputs (constant
+    # test vector, fhe_pbs_gadget_batch), the per-bootstrap yardstick
+    for _ in range(2):
+        eng.pbs_gadget(small, gad, 1 << 62)
+    torch.cuda.synchronize()
+    eng.profile(True)
+    for _ in range(args.steps):
+        eng.pbs_gadget(small, gad, 1 << 62)
+    torch.cuda.synchronize()
+    eng.profile(False)
+    sg = eng.profile_read(bucket)
+    sign_ms = sg["total_ms"] / max(sg["launches"], 1)
+    sign_kernel = eng.kernel_name(bucket)
+    oracle = {}
+    if not args.no_cpu_baseline:
+        from oracle import tfhe_ref as R
+        R.build()
+        ref = R.RefTFHE(p.as_dict(), args.seed)
+        sm = u64(small)[:4]
+        o_ref = ref.pbs_table(sm, lut, lb, gadget=gad)
+        d = (u64(eng.phase(out[:4].contiguous())) - ref.phase(o_ref)).view(np.int64)
+        oracle = {"compares": 4, "decrypt_equal": bool(np.array_equal(ref.decrypt_ints(o_ref), lut[m[:4]])),
+                  "max_phase_diff_log2": round(float(np.log2(max(np.abs(d).max(), 1))), 2)}
+        nthr = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        cnt = 8
+        sm8 = u64(small)[:cnt]
+        t1 = time.perf_counter()
+        ref.pbs_table(sm8, lut, lb, gadget=gad)
+        cpu_s = time.perf_counter() - t1
+        oracle["cpu_baseline"] = {"value": round(cnt / cpu_s, 3), "unit": "PBS/s", "cores": nthr, "kind": "port",
+                                  "sample": f"{cnt} table bootstraps (ref_pbs_table_gadget, exact integer "
+                                            f"restatement, OpenMP over the host cores)"}
+    value = B * args.steps / secs
+    tf = k["achieved_tflops_f64"]
+    line = {
+        "metric": "programmable bootstraps/sec (table PBS, key switch + blind rotation), 1 GPU",
+        "value": round(value, 1), "unit": "PBS/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(secs / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": f"table bootstrap of {B} ciphertexts: {lb}-bit inputs -> {P}-bit outputs "
+                               f"(random signed table), params_for_bits({P}), gadget {gad} ({bl},{lv}) "
+                               f"{'multi-bit' if grp == 2 else 'classic'}",
+                   "ciphertexts": B, "lut_bits": lb, "msg_bits_P": P, "gadget": [bl, lv, grp]},
+        "parity": {"outputs_checked": B, "decrypt_equal_lut": exact, "oracle": oracle},
+        "roofline": {"kernel": k["kernel"], "bound": "f64-valu", "achieved": round(tf, 3),
+                     "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
+                     "traffic": k["hbm_bytes_per_launch"], "flops_per_launch": k["f64_flops_per_launch"],
+                     "flops_source": k["flops_source"], "avg_launch_ms": k["avg_launch_ms"],
+                     "launches": k["launches"], "cts_per_launch": k["cts_per_launch"],
+                     "time_source": "HIP events on the step's launches"},
+        "keyswitch_ms_per_launch": round(ks["total_ms"] / max(ks["launches"], 1), 4),
+        "sign_path_kernel": {"kernel": sign_kernel, "avg_launch_ms": round(sign_ms, 4),
+                             "table_over_sign": round(k["avg_launch_ms"] / sign_ms, 4) if sign_ms else None},
+    }
+    if oracle.get("cpu_baseline"):
+        line["cpu_baseline"] = oracle.pop("cpu_baseline")
+    print(json.dumps(line), flush=True)
 
 
 def corpus_main(args, world, rank, local, dev):

@@ -1289,9 +1289,78 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
                    (hipStream_t)stream);
 }
 
-// The table bootstrap runs on the v2 kernel at N = 1024 (v1 otherwise),
-// instantiated for the wide test-vector argument (BrTvLut); it is not on the
-// compare's hot path, which keeps the v4 kernels' three-word one.
+// The gadget fhe_pbs_table_batch runs on: the most precise (smallest
+// bootstrap variance) multi-bit gadget of the set, whose rotation is the
+// shipped k_blind_rotate_mb / _mb64 family (e.g. (15,2) at P = 16, (5,8) at
+// P = 26); 0 (the classic main gadget, v2 / v1 kernels) when the set has none.
+static int table_gadget(const fhe_params& p) {
+  int best = 0;
+  double v = 0;
+  for (int g = 1; g < NGAD; ++g) {
+    if (!mb_for(p, g)) continue;
+    const double vg = pbs_var(p, gadget_base_log(p, g), gadget_level(p, g), 2);
+    if (!best || vg < v) best = g, v = vg;
+  }
+  return best;
+}
+
+// The table bootstrap on a multi-bit gadget: the sign extraction's kernels
+// (k_blind_rotate_mb: 32-bit accumulators, (23,1) and (15,2) with their base
+// log fixed as there; k_blind_rotate_mb64: 48-bit, levels 2-8) instantiated
+// for the table test vector (BrTvLut), with that gadget's multi-bit key.
+static int launch_br_table_mb(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const BrTvLut& tv, uint64_t* out,
+                              hipStream_t st, int gad) {
+  const fhe_params q = fast_params(ctx->p, gad);
+  const c64* bsk = ctx->bskf_fft[gad - 1];
+  ProfAcc& prof = ctx->prof_brf[gad - 1];
+  hipEvent_t e1;
+  prof_begin(ctx, prof, st, &e1);
+  const char* name = nullptr;
+  const dim3 gm((unsigned)((count + 3) / 4)), bm(v4::nthreads(4));
+#define MBT(L, B)                                                                                                  \
+  do {                                                                                                             \
+    hipLaunchKernelGGL((k_blind_rotate_mb<L, 0, B, BrTvLut>), gm, bm, 0, st, d_small, count, q.n, q.pbs_base_log,   \
+                       bsk, ctx->tw4, ctx->psi, tv, 0, out, nullptr, nullptr, nullptr);                            \
+    name = "k_blind_rotate_mb<" #L ", 0, " #B ", BrTvLut>";                                                        \
+  } while (0)
+#define MB64T(L)                                                                                                   \
+  do {                                                                                                             \
+    hipLaunchKernelGGL((k_blind_rotate_mb64<L, 0, BrTvLut>), gm, bm, 0, st, d_small, count, q.n, q.pbs_base_log,    \
+                       bsk, ctx->tw4, ctx->psi, tv, 0, out, nullptr, nullptr, nullptr);                            \
+    name = "k_blind_rotate_mb64<" #L ", 0, BrTvLut>";                                                              \
+  } while (0)
+  if (q.pbs_level <= 2 && q.pbs_level * q.pbs_base_log <= 31) {
+    if (q.pbs_level == 1) {
+      if (q.pbs_base_log == 23) MBT(1, 23);
+      else MBT(1, 0);
+    } else {
+      if (q.pbs_base_log == 15) MBT(2, 15);
+      else MBT(2, 0);
+    }
+  } else {
+    switch (q.pbs_level) {
+      case 2: MB64T(2); break;
+      case 3: MB64T(3); break;
+      case 4: MB64T(4); break;
+      case 5: MB64T(5); break;
+      case 6: MB64T(6); break;
+      case 7: MB64T(7); break;
+      case 8: MB64T(8); break;
+      default: return fail(ctx, FHE_E_ARG, "table bootstrap: no multi-bit kernel for this gadget level");
+    }
+  }
+#undef MBT
+#undef MB64T
+  prof.kernel = name;
+  prof_end(ctx, prof, st, e1, count);
+  HIPCHK(ctx, hipGetLastError());
+  return FHE_OK;
+}
+
+// The table bootstrap on the classic main gadget (parameter sets without a
+// multi-bit gadget): the v2 kernel at N = 1024 (v1 otherwise), instantiated
+// for the wide test-vector argument (BrTvLut); the compare's hot kernels keep
+// the three-word one.
 static int launch_br_table(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const BrTvLut& tv, uint64_t* out,
                            hipStream_t st) {
   const fhe_params& p = ctx->p;
@@ -1342,16 +1411,32 @@ static int launch_br_table(fhe_ctx* ctx, const uint64_t* d_small, int64_t count,
   return FHE_OK;
 }
 
-int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const int64_t* d_lut, int32_t lut_bits,
-                        uint64_t* d_out, void* stream) {
+int fhe_pbs_table_gadget_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, int32_t gadget,
+                               const int64_t* d_lut, int32_t lut_bits, uint64_t* d_out, void* stream) {
   int rc = need_keys(ctx);
   if (rc) return rc;
   const int logN = log2i(ctx->p.N);
   if (count < 0 || lut_bits < 0 || lut_bits > logN - 1 || !d_lut || (count > 0 && (!d_small || !d_out)))
     return fail(ctx, FHE_E_ARG, "bad pbs-table arguments (0 <= lut_bits <= log2(N) - 1)");
+  if (gadget < 0 || gadget >= NGAD || (gadget > 0 && !mb_for(ctx->p, gadget)))
+    return fail(ctx, FHE_E_ARG, "pbs-table gadget must be 0 (the classic main gadget) or a multi-bit gadget of "
+                                "these parameters");
   if (count == 0) return FHE_OK;
   BrTvLut tv{0, 0, 0, logN - lut_bits, 1 << lut_bits, d_lut, 1ull << (64 - ctx->p.msg_bits)};
+  if (gadget > 0) return launch_br_table_mb(ctx, d_small, count, tv, d_out, (hipStream_t)stream, gadget);
   return launch_br_table(ctx, d_small, count, tv, d_out, (hipStream_t)stream);
+}
+
+int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const int64_t* d_lut, int32_t lut_bits,
+                        uint64_t* d_out, void* stream) {
+  if (!ctx) return fail(nullptr, FHE_E_ARG, "null ctx");
+  return fhe_pbs_table_gadget_batch(ctx, d_small, count, table_gadget(ctx->p), d_lut, lut_bits, d_out, stream);
+}
+
+int fhe_pbs_table_gadget(const fhe_params* params) {
+  std::string why;
+  if (validate(params, why)) return FHE_E_ARG;
+  return table_gadget(*params);
 }
 
 static int ensure_ws(fhe_ctx* ctx, size_t bytes) {

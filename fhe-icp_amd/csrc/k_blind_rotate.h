@@ -738,10 +738,13 @@ __host__ __device__ constexpr int psi_pos(int x) { return x ^ ((x >> 4) & 15); }
 // high 32 bits in acc[] and bits 16-31 of acc[u] and acc[u + S] packed in
 // alo[u] (24 VGPRs instead of 32), each product rounded into them at 2^-48
 // (n (1 + kN/2) 2^-96 / 12 = 2^-80 of variance, below the FFT error).
-template <int L, int DBG, int BETA, int AW>
+// TV: the test vector, the three-word staircase BrTv of the sign extraction
+// or the table BrTvLut of fhe_pbs_table_batch (its own instantiations, so the
+// hot kernels keep the narrow argument)
+template <int L, int DBG, int BETA, int AW, class TV = BrTv>
 __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t count, int n, int beta,
                                           const c64* __restrict__ bsk, const c64* __restrict__ tw4,
-                                          const c64* __restrict__ psi, BrTv tv, int mode, u64* __restrict__ out,
+                                          const c64* __restrict__ psi, TV tv, int mode, u64* __restrict__ out,
                                           u64* __restrict__ ct_v, u64* __restrict__ refreshed, u64* __restrict__ sign) {
   using namespace v4;
   constexpr bool A32 = AW == 1, A48 = AW == 2;
@@ -1069,29 +1072,29 @@ __device__ __forceinline__ void mb_rotate(const u64* __restrict__ small, int64_t
   }
 }
 
-template <int L, int DBG = 0, int BETA = 0>
+template <int L, int DBG = 0, int BETA = 0, class TV = BrTv>
 __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb(const u64* __restrict__ small, int64_t count, int n,
                                                                       int beta, const c64* __restrict__ bsk,
                                                                       const c64* __restrict__ tw4,
-                                                                      const c64* __restrict__ psi, BrTv tv, int mode,
+                                                                      const c64* __restrict__ psi, TV tv, int mode,
                                                                       u64* __restrict__ out, u64* __restrict__ ct_v,
                                                                       u64* __restrict__ refreshed, u64* __restrict__ sign) {
-  mb_rotate<L, DBG, BETA, 1>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
+  mb_rotate<L, DBG, BETA, 1, TV>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
 }
 // the deep gadgets (L * beta > 31) on the multi-bit rotation: 48-bit accumulators
 // (FHEICP_MB64_AW = 0: 64-bit ones, A/B builds)
 #ifndef FHEICP_MB64_AW
 #define FHEICP_MB64_AW 2
 #endif
-template <int L, int DBG = 0>
+template <int L, int DBG = 0, class TV = BrTv>
 __global__ void __launch_bounds__(v4::nthreads(4), 1) k_blind_rotate_mb64(const u64* __restrict__ small, int64_t count,
                                                                         int n, int beta, const c64* __restrict__ bsk,
                                                                         const c64* __restrict__ tw4,
-                                                                        const c64* __restrict__ psi, BrTv tv, int mode,
+                                                                        const c64* __restrict__ psi, TV tv, int mode,
                                                                         u64* __restrict__ out, u64* __restrict__ ct_v,
                                                                         u64* __restrict__ refreshed,
                                                                         u64* __restrict__ sign) {
-  mb_rotate<L, DBG, 0, FHEICP_MB64_AW>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
+  mb_rotate<L, DBG, 0, FHEICP_MB64_AW, TV>(small, count, n, beta, bsk, tw4, psi, tv, mode, out, ct_v, refreshed, sign);
 }
 
 // ---- classic blind rotation with key-stationary products ---------------------

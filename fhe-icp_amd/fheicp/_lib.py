@@ -81,6 +81,8 @@ SIGNATURES = [
     ("fhe_sign_trace_batch", C.c_int, [_CTXP, _vp, _i64, C.POINTER(C.c_int32), _i32, _vp, _vp, _vp]),
     ("fhe_pbs_lut_batch", C.c_int, [_CTXP, _vp, _i64, _u64, _u64, _i32, _vp, _vp]),
     ("fhe_pbs_table_batch", C.c_int, [_CTXP, _vp, _i64, _vp, _i32, _vp, _vp]),
+    ("fhe_pbs_table_gadget_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    ("fhe_pbs_table_gadget", C.c_int, [_P]),
     ("fhe_threshold_batch", C.c_int, [_CTXP, _vp, _i64, _i64, _vp, _vp]),
     ("fhe_compare_batch", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _u64, _u64, _vp, _vp, _vp]),
     ("fhe_compare_batch_key", C.c_int, [_CTXP, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _u64, _vp, _vp, _vp]),

@@ -225,15 +225,25 @@ class Engine:
                                             int(log_slots), _ptr(out), _stream(self.device)))
         return out
 
-    def pbs_table(self, small: torch.Tensor, lut, lut_bits: int) -> torch.Tensor:
-        """Table bootstrap (fhe_pbs_table_batch): input m in [0, 2^lut_bits) at
+    def pbs_table(self, small: torch.Tensor, lut, lut_bits: int, gadget: int | None = None) -> torch.Tensor:
+        """Table bootstrap (fhe_pbs_table_batch; fhe_pbs_table_gadget_batch
+        with an explicit gadget): input m in [0, 2^lut_bits) at
         2^(63 - lut_bits); output lut[m] at 2^(64 - msg_bits)."""
         n = small.numel() // self.Ws
         lut_d = self.to_dev(np.asarray(lut, dtype=np.int64)) if not isinstance(lut, torch.Tensor) else lut
         out = self.empty_big(n)
-        self._chk(self._L.fhe_pbs_table_batch(self._ctx, _ptr(small), n, _ptr(lut_d), int(lut_bits), _ptr(out),
-                                              _stream(self.device)))
+        if gadget is None:
+            rc = self._L.fhe_pbs_table_batch(self._ctx, _ptr(small), n, _ptr(lut_d), int(lut_bits), _ptr(out),
+                                             _stream(self.device))
+        else:
+            rc = self._L.fhe_pbs_table_gadget_batch(self._ctx, _ptr(small), n, int(gadget), _ptr(lut_d),
+                                                    int(lut_bits), _ptr(out), _stream(self.device))
+        self._chk(rc)
         return out
+
+    def table_gadget(self) -> int:
+        """The gadget fhe_pbs_table_batch runs on (fhe_pbs_table_gadget)."""
+        return self._L.fhe_pbs_table_gadget(C.byref(self._P_now()))
 
     def threshold(self, ct_acc: torch.Tensor, T: int) -> torch.Tensor:
         """Encryption of [acc >= T] at 2^63 (fhe_threshold_batch); ct_acc is kept."""

@@ -273,6 +273,15 @@ int fhe_pbs_lut_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, uint
  * half a box. */
 int fhe_pbs_table_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, const int64_t* d_lut, int32_t lut_bits,
                         uint64_t* d_out, void* stream);
+/* fhe_pbs_table_batch on an explicit gadget (0..5, as fhe_pbs_gadget_batch):
+ * a multi-bit gadget runs the sign extraction's multi-bit rotation
+ * (k_blind_rotate_mb / _mb64) with the table test vector and that gadget's
+ * key; 0 the classic main gadget. fhe_pbs_table_batch takes
+ * fhe_pbs_table_gadget(params): the most precise multi-bit gadget of the set
+ * (smallest bootstrap noise), 0 when it has none; FHE_E_ARG on bad params. */
+int fhe_pbs_table_gadget_batch(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, int32_t gadget,
+                               const int64_t* d_lut, int32_t lut_bits, uint64_t* d_out, void* stream);
+int fhe_pbs_table_gadget(const fhe_params* params);
 /* The encrypted decision of batch_operations.py:278 (score >= min_similarity
  * <=> acc >= T, SURVEY.md §8b fhe_threshold_batch): d_ct_acc holds big LWEs of
  * msg_bits-bit accumulators (not modified); d_bit receives the encryption of

@@ -797,6 +797,29 @@ void ref_pbs_table(const ref_params* P, const uint64_t* bsk, const uint64_t* sma
   }
 }
 
+/* ref_pbs_table on gadget g (fhe_pbs_table_gadget_batch): 0 = the classic
+ * main gadget with bsk, 1..5 a gadget of ref_keygen_fast_bsk on the rotation
+ * of its group (the multi-bit one for the shipped table gadgets). */
+void ref_pbs_table_gadget(const ref_params* P0, const uint64_t* bsk, const uint64_t* small, int64_t count, int gadget,
+                          const int64_t* lut, int lut_bits, uint64_t* out) {
+  ref_params P = *P0;
+  int group = 1;
+  if (gadget >= 1 && gadget < NGAD && gadget_level(P0, gadget)) {
+    P.pbs_base_log = gadget_base_log(P0, gadget); P.pbs_level = gadget_level(P0, gadget);
+    group = gadget_group(P0, gadget);
+  }
+#pragma omp parallel
+  {
+    uint64_t* work = (uint64_t*)malloc(8 * pbs_work_words(&P));
+    tv_desc d = {0, 0, 0, lut, 1 << lut_bits, ilog2(P.N) - lut_bits, 0};
+    d.delta = 1ull << (64 - P.msg_bits);
+#pragma omp for schedule(dynamic)
+    for (int64_t c = 0; c < count; ++c)
+      pbs1g(&P, group, bsk, small + (size_t)c * (P.n + 1), &d, out + (size_t)c * (P.k * P.N + 1), work);
+    free(work);
+  }
+}
+
 /* modswitched (a~, b~) of small LWEs, for tests */
 void ref_modswitch(const ref_params* P, const uint64_t* small, int64_t count, uint32_t* out) {
   const int lg = ilog2(2 * P->N);

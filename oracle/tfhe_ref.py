@@ -67,6 +67,7 @@ def lib():
         L.ref_pbs_lut.argtypes = [P, u64p, u64p, C.c_int64, C.c_uint64, C.c_uint64, C.c_int, u64p]
         L.ref_sign_extract.argtypes = [P, u64p, u64p, u64p, C.c_int64, u64p]
         L.ref_pbs_table.argtypes = [P, u64p, u64p, C.c_int64, i64p, C.c_int, u64p]
+        L.ref_pbs_table_gadget.argtypes = [P, u64p, u64p, C.c_int64, C.c_int, i64p, C.c_int, u64p]
         L.ref_sign_extract3.argtypes = [P, u64p, u64p, u64p, u64p, u64p, C.c_int64, u64p]
         L.ref_sign_extract_keys.argtypes = [P, u64p, C.POINTER(u64p), u64p, u64p, C.c_int64, u64p]
         L.ref_sign_schedule.argtypes = [P, C.POINTER(C.c_int32), C.c_int32]; L.ref_sign_schedule.restype = C.c_int
@@ -256,14 +257,20 @@ class RefTFHE:
                           int(log_slots), u64(out))
         return out
 
-    def pbs_table(self, small: np.ndarray, lut, lut_bits: int) -> np.ndarray:
-        """fhe_pbs_table_batch restated (oracle/tfhe_ref.c ref_pbs_table)."""
+    def pbs_table(self, small: np.ndarray, lut, lut_bits: int, gadget: int = 0) -> np.ndarray:
+        """fhe_pbs_table_gadget_batch restated (oracle/tfhe_ref.c
+        ref_pbs_table / ref_pbs_table_gadget): gadget 0 the classic main
+        gadget, else that gadget's key on its group's rotation."""
         small = np.ascontiguousarray(small, dtype=np.uint64)
         lut = np.ascontiguousarray(lut, dtype=np.int64)
         assert lut.size == 1 << lut_bits
         cnt = small.size // (self.n + 1)
         out = np.zeros((cnt, self.big + 1), np.uint64)
-        lib().ref_pbs_table(C.byref(self.P), u64(self.bsk), u64(small), cnt, i64(lut), int(lut_bits), u64(out))
+        if gadget == 0:
+            lib().ref_pbs_table(C.byref(self.P), u64(self.bsk), u64(small), cnt, i64(lut), int(lut_bits), u64(out))
+        else:
+            lib().ref_pbs_table_gadget(C.byref(self.P), u64(self.keys[gadget]), u64(small), cnt, int(gadget), i64(lut),
+                                       int(lut_bits), u64(out))
         return out
 
     def threshold(self, ct_acc: np.ndarray, T: int) -> np.ndarray:

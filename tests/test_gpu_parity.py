@@ -481,7 +481,8 @@ def test_pbs_table_every_value_real(real):
             assert np.array_equal(eng.decrypt(out).cpu().numpy(), lut[m])
             if lut_bits == 4:
                 ref.with_msg_bits(P)
-                o_ref = ref.pbs_table(u64(small)[:4], lut, lut_bits)
+                # the same gadget (fhe_pbs_table_gadget: (15,2) multi-bit here)
+                o_ref = ref.pbs_table(u64(small)[:4], lut, lut_bits, gadget=eng.table_gadget())
                 assert np.array_equal(ref.decrypt_ints(o_ref), lut[m[:4]])
                 d = signed(u64(eng.phase(out[:4].contiguous())) - ref.phase(o_ref))
                 assert np.abs(d).max() < 2 ** 48
@@ -540,3 +541,57 @@ def test_encrypt_linear_fused_bit_exact(which, request):
             continue
         half = 2 ** (eng.msg_bits - 1)
         assert np.array_equal(ref.decrypt_ints(lin_ref), (x @ w + cst + half) % (2 * half) - half)
+
+
+def test_pbs_table_every_multibit_gadget(need_gpu, oracle_lib):
+    """The table bootstrap on every multi-bit gadget of the P = 26 set (mid0
+    (5,8), mid (8,5), mid2 (12,3) on the 48-bit k_blind_rotate_mb64, fast
+    (15,2) and fast2 (23,1) on the 32-bit k_blind_rotate_mb, each with the
+    table test vector and that gadget's key) and on the classic main gadget:
+    a 3-bit table over every input, 16 times each, decrypts exactly at an
+    output width the gadget's noise carries (>= 8 sigma at half a step:
+    26 bits on (5,8) and (6,7), 24 on (8,5), 20 on (12,3), 16 on (15,2), 10
+    on (23,1)); the
+    default gadget is the most precise multi-bit one (mid0); the launched
+    instantiation is the BrTvLut one; on mid0 and fast the phases of four
+    outputs agree with the oracle's ref_pbs_table_gadget to noise level."""
+    p = params_for_bits(26)
+    eng = Engine(p, 0)
+    eng.keygen(8026)
+    ref = None
+    P = p.msg_bits
+    assert eng.table_gadget() == 5
+    lut_bits, M = 3, 8
+    m = np.tile(np.arange(M, dtype=np.int64), 16)
+    eng.set_msg_bits(lut_bits + 1)
+    small = eng.keyswitch(eng.encrypt(m, seed=81), 0, 0)
+    buckets = {1: "fast", 2: "fast2", 3: "mid", 4: "mid2", 5: "mid0"}
+    out_bits = {5: 26, 3: 24, 4: 20, 1: 16, 2: 10, 0: 26}
+    for gad in (5, 3, 4, 1, 2, 0):
+        Po = out_bits[gad]
+        lut = np.random.default_rng(26 + gad).integers(-(2 ** (Po - 1)), 2 ** (Po - 1), M)
+        eng.set_msg_bits(Po)
+        eng.profile(True)
+        out = eng.pbs_table(small, lut, lut_bits, gadget=gad)
+        eng.profile(False)
+        assert np.array_equal(eng.decrypt(out).cpu().numpy(), lut[m]), gad
+        if gad:
+            name = eng.kernel_name(f"blind_rotate_{buckets[gad]}")
+            assert name.endswith("BrTvLut>") and ("mb64<" in name) == (gad in (3, 4, 5)), (gad, name)
+            eng.profile_read(f"blind_rotate_{buckets[gad]}")
+        if gad in (5, 1):
+            if ref is None:   # the oracle's keys of the two gadgets checked (and the main one) only
+                keep = replace(p, pbs_mid_base_log=0, pbs_mid_level=0, pbs_mid_group=0, pbs_mid2_base_log=0,
+                               pbs_mid2_level=0, pbs_mid2_group=0, pbs_fast2_base_log=0, pbs_fast2_level=0,
+                               pbs_fast2_group=0)
+                ref = oracle_lib.RefTFHE(keep.as_dict(), 8026)
+            ref.with_msg_bits(Po)
+            o_ref = ref.pbs_table(u64(small)[:4], lut, lut_bits, gadget=gad)
+            assert np.array_equal(ref.decrypt_ints(o_ref), lut[m[:4]])
+            d = signed(u64(eng.phase(out[:4].contiguous())) - ref.phase(o_ref))
+            assert np.abs(d).max() < 2 ** 48, gad
+    eng.set_msg_bits(P)
+    lut = np.random.default_rng(26).integers(-(2 ** (P - 1)), 2 ** (P - 1), M)
+    out = eng.pbs_table(small, lut, lut_bits)       # the default: mid0
+    assert np.array_equal(eng.decrypt(out).cpu().numpy(), lut[m])
+    eng.close()

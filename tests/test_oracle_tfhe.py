@@ -356,6 +356,14 @@ def test_oracle_pbs_table_every_value(oracle_lib, lut_bits):
     ref.with_msg_bits(P_out)
     out = ref.pbs_table(small, lut, lut_bits)
     assert np.array_equal(ref.decrypt_ints(out), lut)
+    # the multi-bit table bootstrap (fhe_pbs_table_gadget_batch on a
+    # multi-bit gadget): the same table through ref_pbs_table_gadget
+    prm_mb = replace(prm, pbs_fast_base_log=15, pbs_fast_level=2, pbs_fast_group=2)
+    ref_mb = oracle_lib.RefTFHE(prm_mb.as_dict(), 99)
+    small = ref_mb.keyswitch(ref_mb.encrypt_ints(m, seed=6))
+    ref_mb.with_msg_bits(P_out)
+    out_mb = ref_mb.pbs_table(small, lut, lut_bits, gadget=1)
+    assert np.array_equal(ref_mb.decrypt_ints(out_mb), lut)
 
 
 def test_oracle_threshold_restatement(oracle_lib):
