@@ -44,6 +44,7 @@ import torch  # noqa: E402
 METRIC = "encrypted compares/sec (PBS/sec), 16-dim, 1/2/4/8 GPU; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
 F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector peak (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
+PEAK_CLOCK_MHZ = 2400.0        # the clock F64_VALU_PEAK_TFLOPS is quoted at
 # PMC measurement of this build's blind-rotation kernels (tools/pmc_bench.sh ->
 # tools/br_pmc.py): executed f64 FLOPs and HBM bytes per launch, keyed on the
 # sha256 of the libfheicp.so they were measured on
@@ -269,6 +270,10 @@ def _br_kernel(q, br, pmc, group: int = 1) -> dict:
         "achieved_gbs": alg_bytes / secs / 1e9 if br["launches"] else 0.0,
         # HBM bytes do not scale with the batch (each XCD's L2 streams the key once): exact batch only
         "hbm_bytes_per_launch": float(m["hbm_bytes_per_launch"]) if "hbm_bytes_per_launch" in m else None,
+        # the clock the kernel held in the PMC pass (GRBM_GUI_ACTIVE / 8 XCDs /
+        # dispatch time): the f64-heavy kernels run below the 2.4 GHz the peak
+        # is quoted at (power), so frac_at_clock prices them at their own clock
+        "clock_mhz": (anyk or {}).get("clock_mhz"),
         "pmc_avg_launch_ms": m.get("avg_launch_ms"),
         "pmc_command": (anyk or {}).get("command"),
     }
@@ -368,6 +373,7 @@ def roofline(p, brs, batch: int = 0, iso: dict | None = None) -> dict:
             ks[g]["launches"] = brs[g]["launches"]
     k = ks[dom]
     tf = k["achieved_tflops_f64"]
+    clk = k.get("clock_mhz")
     return {
         "kernel": k["kernel"],
         "bound": "f64-valu",
@@ -375,6 +381,8 @@ def roofline(p, brs, batch: int = 0, iso: dict | None = None) -> dict:
         "peak": F64_VALU_PEAK_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
+        "clock_mhz": clk,
+        "frac_at_clock": round(tf / (F64_VALU_PEAK_TFLOPS * clk / PEAK_CLOCK_MHZ), 4) if clk else None,
         "traffic": k["hbm_bytes_per_launch"],
         "flops_per_launch": k["f64_flops_per_launch"],
         # a pipelined step runs two half-batch launches at once, so its
@@ -884,6 +892,9 @@ def lut_main(args, world, rank, local, dev):
                      "traffic": k["hbm_bytes_per_launch"], "flops_per_launch": k["f64_flops_per_launch"],
                      "flops_source": k["flops_source"], "avg_launch_ms": k["avg_launch_ms"],
                      "launches": k["launches"], "cts_per_launch": k["cts_per_launch"],
+                     "clock_mhz": k["clock_mhz"],
+                     "frac_at_clock": round(tf / (F64_VALU_PEAK_TFLOPS * k["clock_mhz"] / PEAK_CLOCK_MHZ), 4)
+                     if k["clock_mhz"] else None,
                      "time_source": "HIP events on the step's launches"},
         "keyswitch_ms_per_launch": round(ks["total_ms"] / max(ks["launches"], 1), 4),
         "sign_path_kernel": {"kernel": sign_kernel, "avg_launch_ms": round(sign_ms, 4),

@@ -8,6 +8,7 @@ Inputs: rocprofv3 counter_collection.csv files of separate --pmc passes over
   f64   SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU
   fetch FETCH_SIZE
   write WRITE_SIZE
+  grbm  GRBM_GUI_ACTIVE GRBM_COUNT (the clock each kernel held)
 and the kernel-trace csv of the same command for the per-launch durations.
 Recipe (MI355X_MICROARCH.md, HBM/rocprofv3): SQ_INSTS_* count wave64
 instructions, so f64 FLOPs = 64 x (2 FMA + ADD + MUL); FETCH_SIZE/WRITE_SIZE
@@ -40,6 +41,25 @@ def per_kernel(path, match=("k_blind_rotate", "k_keyswitch", "k_encrypt_linear")
     return {n: {c: (sum(v) / len(v), len(v)) for c, v in cs.items()} for n, cs in acc.items()}
 
 
+def grbm_clock(path, xcds=8):
+    """Per kernel: GRBM_GUI_ACTIVE per dispatch (summed over the XCDs) over
+    the dispatch's own duration in that pass -> the clock the kernel held,
+    MHz. The counter window is a few microseconds longer than the dispatch,
+    so for a kernel of tens of microseconds this is an upper bound; for the
+    millisecond blind rotations it is the clock."""
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != "GRBM_GUI_ACTIVE":
+            continue
+        n = kname(r["Kernel_Name"])
+        dur_us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+        if dur_us > 0:
+            d[n].append((float(r["Counter_Value"]), dur_us))
+    return {n: {"grbm_gui_active_per_launch": sum(g for g, _ in v) / len(v),
+                "grbm_window_us": sum(t for _, t in v) / len(v),
+                "clock_mhz": sum(g for g, _ in v) / xcds / sum(t for _, t in v)} for n, v in d.items()}
+
+
 def trace_ms(path):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -56,12 +76,14 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--trace", default="")
+    ap.add_argument("--grbm", default="", help="counter csv of a GRBM_GUI_ACTIVE GRBM_COUNT pass")
     ap.add_argument("--command", default="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline")
     ap.add_argument("--out", required=True)
     ap.add_argument("--merge", default="", help="an earlier br_pmc.json of the same library to extend")
     a = ap.parse_args()
     f64, fetch, write = per_kernel(a.f64), per_kernel(a.fetch), per_kernel(a.write)
     tr = trace_ms(a.trace) if a.trace else {}
+    clk = grbm_clock(a.grbm) if a.grbm else {}
     sha = hashlib.sha256(open(a.lib, "rb").read()).hexdigest()
     out = {"lib_sha256": sha, "commands": [], "kernels": {}}
     if a.merge:
@@ -88,6 +110,8 @@ def main():
             e.update(fetch_size_kib=fk, write_size_kib=wk, hbm_bytes_per_launch=(2 * fk + wk) * 1024)
         if n in tr:
             e["avg_launch_ms"], e["trace_launches"] = tr[n]
+        if n in clk:
+            e.update({k: round(v, 1) for k, v in clk[n].items()})
         out["kernels"][f"{n}@{a.cts}"] = e
     s = json.dumps(out, indent=1)
     open(a.out, "w").write(s + "\n")

@@ -1,6 +1,6 @@
 #!/bin/bash
-# PMC + kernel-trace passes of the headline, C3 (one stream: FHEICP_PIPE=0)
-# and C5 runs of this build, merged into one br_pmc.json keyed on its sha
+# PMC + kernel-trace passes of the headline, C3 (one stream: FHEICP_PIPE=0),
+# C5 and the table-bootstrap (--mode lut) runs of this build, merged into one br_pmc.json keyed on its sha
 # (copy gpurun_out/pmc_r03/br_pmc.json to profiles/br_pmc.json), and each
 # run's rocprofv3 --stats kernel summary.
 set -u -o pipefail
@@ -18,3 +18,5 @@ export FHEICP_PIPE=0
 PMC_ENV="FHEICP_PIPE=0 " run c3 10000 --docs 10000 --dim 32 --n-bits 8 || exit 1
 unset FHEICP_PIPE
 run c5 1000 --docs 1000 --dim 768 --n-bits 8 || exit 1
+# the table bootstrap on the multi-bit rotation (bench.py --mode lut)
+run lut 1024 --mode lut || exit 1
