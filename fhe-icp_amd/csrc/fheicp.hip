@@ -845,7 +845,9 @@ static int encrypt_linear_impl(fhe_ctx* ctx, const int64_t* d_qx, int64_t B, int
   hipEvent_t e1;
   prof_begin(ctx, ctx->prof_enc, (hipStream_t)stream, &e1);
   ctx->prof_enc.kernel = "k_encrypt_linear";
-  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(EL_THREADS), (size_t)p.k * p.N * 8, (hipStream_t)stream, K, p.N,
+  // the chunk's mask in its E form (k_client.h el_region): k * 2N * 9 / 8 words
+  hipLaunchKernelGGL(k_encrypt_linear, dim3((unsigned)B), dim3(EL_THREADS), (size_t)p.k * el_region(p.N) * 8,
+                     (hipStream_t)stream, K, p.N,
                      p.k, p.msg_bits, p.glwe_noise_bits, ctx->s_big, d_qx, (int)D, G, d_w,
                      ((u64)cst) << (64 - p.msg_bits), id0, d_out);
   prof_end(ctx, ctx->prof_enc, (hipStream_t)stream, e1, B);

@@ -278,6 +278,44 @@ __device__ __forceinline__ void packed_chunk_mask(const u64* A, int N, int k, co
   }
 }
 
+// k_encrypt_linear's LDS form of a chunk's mask: per component i, Ahat_i over
+// m in [-N, N) stored at e = m + N, so the negacyclic sign is in the data
+// (E[e] = -A[e] for e < N, A[e - N] from N on) and a window read is a plain
+// load; one pad word per 8 (physical e + e / 8), so the lanes' windows,
+// 8 words apart, start 9 words apart: 2-way instead of 16-way LDS bank
+// conflicts. 2N * 9 / 8 words per component.
+__host__ __device__ __forceinline__ constexpr int el_region(int N) { return 2 * N / 8 * 9; }
+// mask block blk (words [8 blk, 8 blk + 8) of the chunk's kN mask words) into E
+__device__ __forceinline__ void el_store_block(u64* E, int N, int blk, const u64 m[8]) {
+  const int i = 8 * blk / N, b = blk - i * (N / 8);
+  u64* pos = E + i * el_region(N) + 9 * (N / 8 + b);
+  u64* neg = E + i * el_region(N) + 9 * b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    pos[j] = m[j];
+    neg[j] = (u64)0 - m[j];
+  }
+}
+// packed_mac8 on the E form: acc[r] += sum_{t < Dg} w[t] Ahat[t - u0 - r]; the
+// window of iteration j0 is E[e0 + q], e0 = N - u0 - 7 + j0 = 8 b0 + 1, read
+// fresh (15 words, constant offsets from one per-lane base advancing 9 words
+// per iteration); the weights are wave-uniform, loaded into scalar registers
+__device__ __forceinline__ void packed_mac8_e(const u64* E, int N, int u0, const int64_t* __restrict__ w, int Dg,
+                                              u64 acc[8]) {
+  const u64* p = E + 9 * (N / 8 - u0 / 8 - 1);
+  for (int j0 = 0; j0 < Dg; j0 += 8, p += 9) {
+    u64 win[15];
+#pragma unroll
+    for (int q = 0; q < 15; ++q) win[q] = p[1 + q + ((1 + q) >> 3)];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const u64 wj = j0 + jj < Dg ? (u64)w[j0 + jj] : 0;  // past Dg: those features weigh nothing
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] += wj * win[jj + 7 - r];
+    }
+  }
+}
+
 // Server side: the leveled dot product over packed GLWE inputs
 // (fhe_linear_packed_batch): out[b] = sum_g Extract_0(GLWE_g W_g) +
 // trivial(cst Delta). One workgroup per pair, A of each chunk staged in LDS.
@@ -390,8 +428,10 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
     if ((wv + 1) * 64 <= nblk && 8 * wv < Dg) {
       uint32_t o[16], e4[4];
       chacha20_block_with_quad(K, (uint32_t)blk, TAG_ENC_MASK, id, o, (uint32_t)nb, TAG_ENC_NOISE, id, q, e4);
+      u64 m[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) shm[8 * blk + j] = (u64)o[2 * j] | ((u64)o[2 * j + 1] << 32);
+      for (int j = 0; j < 8; ++j) m[j] = (u64)o[2 * j] | ((u64)o[2 * j + 1] << 32);
+      el_store_block(shm, N, blk, m);
       if (8 * nb < Dg) noise_words(nb, e4);
       blk += 256;
       nb += 64;
@@ -399,8 +439,7 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
     for (; blk < nblk; blk += 256) {
       u64 m[8];
       stream_block(K, TAG_ENC_MASK, id, (uint32_t)blk, m);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) shm[8 * blk + j] = m[j];
+      el_store_block(shm, N, blk, m);
     }
     EL_STAMP(2, __builtin_amdgcn_s_memtime());
     for (; 8 * nb < Dg; nb += 64) {
@@ -411,7 +450,10 @@ __global__ void __launch_bounds__(EL_THREADS) k_encrypt_linear(ChaKey K, int N, 
     EL_STAMP(3, __builtin_amdgcn_s_memtime());
     __syncthreads();
     EL_STAMP(4, __builtin_amdgcn_s_memtime());
-    packed_chunk_mask(shm, N, k, w + g * N, Dg, acc);
+    if (t8 < k * N) {
+      const int i = t8 / N;
+      packed_mac8_e(shm + i * el_region(N), N, t8 - i * N, w + g * N, Dg, acc);
+    }
     EL_STAMP(5, __builtin_amdgcn_s_memtime());
   }
   u64* o = out + (size_t)b * (k * N + 1);
