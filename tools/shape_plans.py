@@ -15,7 +15,11 @@ products: (k+1)^2 L complex MACs per point classic, 3 (k+1)^2 L + 3 (k+1) per
 pair multi-bit, 8 flops each). A key-switch cost is added per bootstrap:
 0.017 x (level / 5) of the L = 2 classic rotation (k_keyswitch_mfma).
 No GPU; prints a markdown table.
-Usage: tools/shape_plans.py [P ...]"""
+With --probe FILE (the output of tools/shape_probe.hip) the k = 1 costs come
+from the measured ns per transform point and per complex MAC instead of the
+counted flops (--probe-waves 2 or 3: the occupancy the k = 1 kernel is priced
+at).
+Usage: tools/shape_plans.py [--probe FILE [--probe-waves W]] [P ...]"""
 from __future__ import annotations
 
 import itertools
@@ -41,10 +45,49 @@ def flops_per_coef(k: int, N: int, L: int, grp: int) -> float:
     return ((k + 1) * (L + 1) * M * ct + (3 * (k + 1) ** 2 * L + 3 * (k + 1)) * M * 8) / 2
 
 
+# measured per-point costs (tools/shape_probe.hip, ns per point per SIMD):
+# set by --probe FILE; None = the counted flops above
+PROBE = None
+
+
+def parse_probe(path: str) -> dict:
+    """ns per transform point (fwd + inv pair) at M = 512 / 1024 and per
+    complex MAC, at 3 and 2 waves per SIMD, from the probe's output."""
+    import re
+    out = {}
+    for ln in open(path):
+        m = re.match(r"(\d+)-pt fwd\+inv, (\d) waves/SIMD.*?([\d.]+) ns per pt", ln)
+        if m:
+            out[("T", int(m.group(1)), int(m.group(2)))] = float(m.group(3))
+        m = re.match(r"cmac .*?(\d) w/SIMD.*?([\d.]+) ns per cmac", ln)
+        if m:
+            out[("mac", int(m.group(1)))] = float(m.group(2))
+    return out
+
+
+def cost_per_pair_measured(k: int, N: int, L: int, grp: int, waves: int) -> float:
+    """Probe-priced work per LWE coefficient: (k+1)(L+1) forward + inverse
+    transform halves of M points at the measured ns per point, and the
+    products' complex MACs at the measured ns per MAC (multi-bit: per pair,
+    halved per coefficient)."""
+    M = N // 2
+    t_T = PROBE[("T", M, waves)] / 2.0      # the probe prices a forward + inverse pair
+    t_mac = PROBE[("mac", waves)]
+    if grp == 1:
+        return (k + 1) * (L + 1) * M * t_T + (k + 1) ** 2 * L * M * t_mac
+    return ((k + 1) * (L + 1) * M * t_T + (3 * (k + 1) ** 2 * L + 3 * (k + 1)) * M * t_mac) / 2
+
+
+# the occupancy a k = 1, N = 2048 kernel is priced at (--probe-waves)
+K1_WAVES = 2
+
+
 def br_cost(k: int, N: int, L: int, grp: int) -> float:
     base = BR_COST[(L, grp)]
     if (k, N) == (2, 1024):
         return base
+    if PROBE:
+        return base * cost_per_pair_measured(k, N, L, grp, K1_WAVES) / cost_per_pair_measured(2, 1024, L, grp, 3)
     return base * flops_per_coef(k, N, L, grp) / flops_per_coef(2, 1024, L, grp)
 
 
@@ -86,7 +129,25 @@ def best_plan(p: SchemeParams, d: int):
 
 
 def main():
-    Ps = [int(x) for x in sys.argv[1:]] or [16, 21, 26]
+    global PROBE, K1_WAVES
+    args = sys.argv[1:]
+    if "--probe" in args:
+        i = args.index("--probe")
+        PROBE = parse_probe(args[i + 1])
+        del args[i:i + 2]
+    if "--probe-waves" in args:
+        i = args.index("--probe-waves")
+        K1_WAVES = int(args[i + 1])
+        del args[i:i + 2]
+    Ps = [int(x) for x in args] or [16, 21, 26]
+    if PROBE:
+        print(f"costs: measured (tools/shape_probe.hip), k = 1 priced at {K1_WAVES} waves/SIMD; "
+              f"probe: " + ", ".join(f"{k}: {v}" for k, v in sorted(PROBE.items(), key=str)))
+        for L in (1, 2, 3, 5, 8):
+            print(f"  L = {L} multi-bit: k=1,N=2048 / k=2,N=1024 work per coefficient = "
+                  f"{br_cost(1, 2048, L, 2) / BR_COST[(L, 2)]:.3f} (counted flops: "
+                  f"{flops_per_coef(1, 2048, L, 2) / flops_per_coef(2, 1024, L, 2):.3f})")
+        print()
     print("| P | shape (k, N) | key switch | d | PBS | plan (base_log, level, group) | relative cost |")
     print("|---|---|---|---|---|---|---|")
     summary = {}
