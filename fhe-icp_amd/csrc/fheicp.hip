@@ -1167,7 +1167,7 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
 #define MB64(L)                                                                                                  \
   hipLaunchKernelGGL((k_blind_rotate_mb64<L, 0>), gm, bm, 0, st, d_small, count, p.n, p.pbs_base_log, bsk_fft,   \
                      ctx->tw4, ctx->psi, tv, mode, out, ct_v, refreshed, sign);                                 \
-  name = "k_blind_rotate_mb64<" #L ", 0>"
+  name = "k_blind_rotate_mb64<" #L ", 0, BrTv>"
       switch (p.pbs_level) {
         case 1: MB64(1); break;
         case 2: MB64(2); break;
@@ -1184,16 +1184,16 @@ static int launch_br(fhe_ctx* ctx, const uint64_t* d_small, int64_t count, BrTv 
     // the shipped fast gadgets (23,1) and (15,2) with their base log fixed
     if (p.pbs_level == 1 && p.pbs_base_log == 23) {
       MBD(1, 0, 23);
-      name = "k_blind_rotate_mb<1, 0, 23>";
+      name = "k_blind_rotate_mb<1, 0, 23, BrTv>";
     } else if (p.pbs_level == 1) {
       MBD(1, 0, 0);
-      name = "k_blind_rotate_mb<1, 0, 0>";
+      name = "k_blind_rotate_mb<1, 0, 0, BrTv>";
     } else if (p.pbs_base_log == 15) {
       MBD(2, 0, 15);
-      name = "k_blind_rotate_mb<2, 0, 15>";
+      name = "k_blind_rotate_mb<2, 0, 15, BrTv>";
     } else {
       MBD(2, 0, 0);
-      name = "k_blind_rotate_mb<2, 0, 0>";
+      name = "k_blind_rotate_mb<2, 0, 0, BrTv>";
     }
 #undef MBD
   } else if (p.N == 1024 && p.k == 2 && var == 4 && !v4_a32(ctx, p)) {

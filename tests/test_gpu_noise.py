@@ -40,21 +40,21 @@ INSTANCES = {
     (7, 6, 1): "k_blind_rotate_v4s<6, false, 0, 0>",
     (6, 7, 1): "k_blind_rotate_v4s<7, false, 0, 0>",
     (5, 8, 1): "k_blind_rotate_v4s<8, false, 0, 0>",
-    (15, 2, 2): "k_blind_rotate_mb<2, 0, 15>",
-    (23, 1, 2): "k_blind_rotate_mb<1, 0, 23>",
+    (15, 2, 2): "k_blind_rotate_mb<2, 0, 15, BrTv>",
+    (23, 1, 2): "k_blind_rotate_mb<1, 0, 23, BrTv>",
     # the multi-bit kernels with a run-time base log (other gadgets)
-    (14, 2, 2): "k_blind_rotate_mb<2, 0, 0>",
-    (22, 1, 2): "k_blind_rotate_mb<1, 0, 0>",
+    (14, 2, 2): "k_blind_rotate_mb<2, 0, 0, BrTv>",
+    (22, 1, 2): "k_blind_rotate_mb<1, 0, 0, BrTv>",
     # the deep gadgets on the multi-bit rotation, 48-bit accumulators
-    (12, 3, 2): "k_blind_rotate_mb64<3, 0>",
-    (10, 4, 2): "k_blind_rotate_mb64<4, 0>",
-    (8, 5, 2): "k_blind_rotate_mb64<5, 0>",
-    (7, 6, 2): "k_blind_rotate_mb64<6, 0>",
-    (6, 7, 2): "k_blind_rotate_mb64<7, 0>",
-    (5, 8, 2): "k_blind_rotate_mb64<8, 0>",
+    (12, 3, 2): "k_blind_rotate_mb64<3, 0, BrTv>",
+    (10, 4, 2): "k_blind_rotate_mb64<4, 0, BrTv>",
+    (8, 5, 2): "k_blind_rotate_mb64<5, 0, BrTv>",
+    (7, 6, 2): "k_blind_rotate_mb64<6, 0, BrTv>",
+    (6, 7, 2): "k_blind_rotate_mb64<7, 0, BrTv>",
+    (5, 8, 2): "k_blind_rotate_mb64<8, 0, BrTv>",
     # level 2 with L * beta > 31 also takes the 48-bit kernel (level 1 would
     # need beta >= 32, which fhe_ctx_create refuses for multi-bit gadgets)
-    (16, 2, 2): "k_blind_rotate_mb64<2, 0>",
+    (16, 2, 2): "k_blind_rotate_mb64<2, 0, BrTv>",
 }
 COUNT = 4096
 TV = 1 << 61
