@@ -202,6 +202,21 @@ def _gadget_var(p: "SchemeParams", g: int) -> float:
     return _variances(replace(p, pbs_base_log=bl, pbs_level=lv), group=grp)[0]
 
 
+def table_gadget(p: "SchemeParams") -> int:
+    """The gadget fhe_pbs_table_batch runs on (fheicp.hip table_gadget): the
+    multi-bit gadget of the set with the smallest bootstrap noise (first on a
+    tie, in gadget order), 0 (the classic main gadget) when it has none."""
+    groups = (p.pbs_fast_group, p.pbs_fast2_group, p.pbs_mid_group, p.pbs_mid2_group, p.pbs_mid0_group)
+    best, v = 0, 0.0
+    for g in range(1, 6):
+        if not gadget_level(p, g) or groups[g - 1] != 2:
+            continue
+        vg = _gadget_var(p, g)
+        if not best or vg < v:
+            best, v = g, vg
+    return best
+
+
 def _sched_worst(p: "SchemeParams", d: int, sched) -> float:
     """Worst decision margin (sigmas) when bootstrap r runs on gadget
     sched[r] (fheicp.hip plan_worst); round r's modulus switch is that of its

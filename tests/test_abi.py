@@ -315,3 +315,20 @@ def test_params_struct_size_refuses_stale_bindings():
     got = _lib.FheParams()
     assert L.fhe_get_params(h, C.byref(got)) == 0 and got.struct_size == P.struct_size
     L.fhe_ctx_destroy(h)
+
+
+def test_table_gadget_matches_params():
+    """fhe_pbs_table_gadget (the gadget the table bootstrap runs on) agrees
+    with params.table_gadget on every planned width and TOY: (15,2) multi-bit
+    at P = 16, mid0 (5,8) at P = 26, the classic main gadget on TOY."""
+    from fheicp.params import table_gadget
+    L = _lib.lib()
+    for P in list(range(4, 28)):
+        p = params_for_bits(P)
+        cp = _lib.params_struct(p.as_dict())
+        assert L.fhe_pbs_table_gadget(C.byref(cp)) == table_gadget(p), P
+    assert table_gadget(params_for_bits(16)) == 1
+    assert table_gadget(params_for_bits(26)) == 5
+    assert L.fhe_pbs_table_gadget(C.byref(_lib.params_struct(TOY.as_dict()))) == table_gadget(TOY) == 0
+    bad = _lib.params_struct(dict(TOY.as_dict(), N=1000))
+    assert L.fhe_pbs_table_gadget(C.byref(bad)) == -1
