@@ -245,8 +245,27 @@ static double pbs_var(const fhe_params& p, int beta, int L, int group = 1) {
   const double arith = group == 2 ? 3.0 * fft + 0.5 * out32 : fft + out32;
   return km * p.n * rows * (B * B + 2) / 12.0 * s2_bsk + steps / (12.0 * std::pow(B, 2.0 * L)) + steps * arith;
 }
+// the key switch's KSK words are rounded to multiples of 2^R (k_server.h
+// ks_round): R = 8 floor((lwe_noise_bits - 6) / 8), so the rounding's
+// 2^R / sqrt(12) stays below 2^-7 of the KSK noise TUniform(lwe_noise_bits)
+// and the i8 MFMA key switch runs on 8 - R / 8 byte planes (3 at the shipped
+// lwe_noise_bits = 46; R at most 40). oracle/tfhe_ref.c ks_round_bits and
+// params.ks_round_bits agree.
+static int ks_round_bits(const fhe_params& p) {
+  return p.lwe_noise_bits < 14 ? 0 : 8 * std::min((p.lwe_noise_bits - 6) / 8, 5);
+}
+// the MFMA key switch's column blocks per workgroup (k_keyswitch_mfma CB):
+// three when the rounded key has at most 4 byte planes, and the 16-column
+// blocks of the key planes padded to a multiple of it (zero columns)
+static int ks_cb(const fhe_params& p) { return 8 - ks_round_bits(p) / 8 <= 4 ? 3 : 1; }
+static int ks_nb(const fhe_params& p) {
+  const int cb = ks_cb(p), nb = (p.n + 1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
+  return (nb + cb - 1) / cb * cb;
+}
 static double ks_var(const fhe_params& p) {
-  const double s2_ksk = tuniform_var(p.lwe_noise_bits) / std::ldexp(1.0, 128);
+  const int R = ks_round_bits(p);
+  const double s2_ksk = (tuniform_var(p.lwe_noise_bits) + (R ? std::ldexp(1.0, 2 * R) / 12.0 : 0.0)) /
+                        std::ldexp(1.0, 128);
   const double Bk = std::ldexp(1.0, p.ks_base_log);
   return (double)p.k * p.N * p.ks_level * (Bk * Bk + 2) / 12.0 * s2_ksk +
          p.k * p.N / 2.0 * std::ldexp(1.0, -2 * p.ks_level * p.ks_base_log) / 12.0;
@@ -653,14 +672,15 @@ static int convert_bsk(fhe_ctx* ctx, hipStream_t st) {
     HIPCHK(ctx, hipFree(ctx->bsk_fft_v2));
     ctx->bsk_fft_v2 = nullptr;
   }
+  const int R = ks_round_bits(p);
   hipLaunchKernelGGL(k_ksk_colsum, dim3((p.n + 1 + 255) / 256), dim3(256), 0, st, ctx->ksk, p.k * p.N * p.ks_level,
-                     p.n, ctx->ksk_colsum);
+                     p.n, R, ctx->ksk_colsum);
   if (ctx->ks_variant == 2) {
-    const int K = p.k * p.N * p.ks_level, n1 = p.n + 1, NB = (n1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
-    if (!ctx->ksk8) HIPCHK(ctx, hipMalloc(&ctx->ksk8, (size_t)K * NB * 16 * 8));
+    const int K = p.k * p.N * p.ks_level, n1 = p.n + 1, NB = ks_nb(p);
+    if (!ctx->ksk8) HIPCHK(ctx, hipMalloc(&ctx->ksk8, (size_t)K * NB * 16 * (8 - R / 8)));
     const int64_t tot = (int64_t)K * NB * 16;
     hipLaunchKernelGGL(k_ksk_to_i8, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ctx->ksk, K, p.k * p.N,
-                       p.ks_level, n1, NB, ctx->ksk8);
+                       p.ks_level, n1, NB, R, 8 - R / 8, ctx->ksk8);
   }
   bsk_to_fft(ctx, p, ctx->bsk, ctx->bsk_fft, st);
   for (int g = 1; g < NGAD; ++g)
@@ -1002,7 +1022,7 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
   const int64_t tiles = (count + KS_TC - 1) / KS_TC;
   if (tiles > 65535) return fail(ctx, FHE_E_ARG, "keyswitch batch too large: split the call");
   if (ctx->ks_variant == 2) {
-    const int K = p.k * p.N * p.ks_level, KB = K / 64, n1 = p.n + 1, NB = (n1 + KSM_NB_COLS - 1) / KSM_NB_COLS;
+    const int K = p.k * p.N * p.ks_level, KB = K / 64, n1 = p.n + 1, NB = ks_nb(p), CB = ks_cb(p);
     const int64_t ncb = (count + 15) / 16;
     const size_t dbytes = (size_t)ncb * 16 * K;
     int rc = ks_reserve(ctx, count, lane);
@@ -1016,8 +1036,28 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
     ctx->prof_ks.kernel = "k_keyswitch_mfma";
     hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)(p.k * p.N / 64), (unsigned)ncb), dim3(256), 0, st, d_big, count,
                        p.k * p.N, p.ks_base_log, p.ks_level, shift, add_body, KB, D, body);
-    hipLaunchKernelGGL(k_keyswitch_mfma, dim3((unsigned)(((count + KSM_CTS - 1) / KSM_CTS) * NB)), dim3(256), 0, st,
-                       (const v4i*)D, (const v4i*)ctx->ksk8, body, count, n1, NB, KB, d_small);
+    const int R = ks_round_bits(p);
+    // K split over S workgroups when the (ciphertext block, column group)
+    // grid alone would leave CUs idle: ~2 workgroups per CU
+    const int64_t ctb = (count + KSM_CTS - 1) / KSM_CTS, tiles = ctb * (NB / CB);
+    int S = (int)std::max<int64_t>(1, std::min<int64_t>(KB / KSM_RING, 512 / tiles));
+    const int kslice = (KB / KSM_RING + S - 1) / S * KSM_RING;
+    S = (KB + kslice - 1) / kslice;
+    if (S > 1) HIPCHK(ctx, hipMemsetAsync(d_small, 0, 8 * (size_t)count * n1, st));
+    const dim3 gks((unsigned)(tiles * S));
+#define KSM(Q, C)                                                                                                    \
+  hipLaunchKernelGGL((k_keyswitch_mfma<Q, C>), gks, dim3(256), 0, st, (const v4i*)D, (const v4i*)ctx->ksk8, body,    \
+                     count, n1, NB, KB, R, S, kslice, d_small)
+    switch ((8 - R / 8) * 4 + CB) {
+      case 3 * 4 + 3: KSM(3, 3); break;
+      case 4 * 4 + 3: KSM(4, 3); break;
+      case 5 * 4 + 1: KSM(5, 1); break;
+      case 6 * 4 + 1: KSM(6, 1); break;
+      case 7 * 4 + 1: KSM(7, 1); break;
+      case 8 * 4 + 1: KSM(8, 1); break;
+      default: return fail(ctx, FHE_E_ARG, "key-switch byte planes out of range");
+    }
+#undef KSM
     prof_end(ctx, ctx->prof_ks, st, e1, count);
     HIPCHK(ctx, hipGetLastError());
     return FHE_OK;
@@ -1028,7 +1068,7 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
   ctx->prof_ks.kernel = "k_keyswitch";
   hipLaunchKernelGGL(k_keyswitch, dim3((p.n + 1 + 255) / 256, (unsigned)tiles, KS_SPLIT), dim3(256), 0, st, d_big,
                      count, p.k * p.N, p.n, p.ks_level, p.ks_base_log, shift, add_body, ctx->ksk, ctx->ksk_colsum,
-                     d_small);
+                     ks_round_bits(p), d_small);
   prof_end(ctx, ctx->prof_ks, st, e1, count);
   HIPCHK(ctx, hipGetLastError());
   return FHE_OK;

@@ -19,6 +19,14 @@ __global__ void __launch_bounds__(256) k_linear(const u64* __restrict__ ct, int 
   out[(size_t)b * W + t] = acc;
 }
 
+// The key switch uses every KSK word rounded to a multiple of 2^R (R =
+// ks_round_bits): the rounding error (2^R / sqrt(12)) is
+// 2^-7 of the KSK's own noise, and the i8 MFMA form then needs 8 - R / 8
+// byte planes instead of 8.
+__device__ __forceinline__ u64 ks_round(u64 x, int R) {
+  return R ? (x + (1ull << (R - 1))) & ~((1ull << R) - 1) : x;
+}
+
 // Key switch (big -> small key), as a split-K integer GEMM:
 //   out[c][t] = body_c + (B/2) colsum[t] - sum_{i,l} d'[c][i][l] * KSK[i][l][t]
 // with offset-binary digits d' = d + B/2 in [0, B) (so each term is two
@@ -31,7 +39,7 @@ constexpr int KS_TC = 16, KS_IC = 32, KS_SPLIT = 8;
 __global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, int64_t count, int big, int n,
                                                    int KL, int kbeta, int shift, u64 add_body,
                                                    const u64* __restrict__ ksk, const u64* __restrict__ colsum,
-                                                   u64* __restrict__ out) {
+                                                   int R, u64* __restrict__ out) {
   __shared__ uint8_t dig[KS_IC][8][KS_TC];  // [input][level][ciphertext]
   const int col = blockIdx.x * 256 + threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.y * KS_TC;
@@ -70,7 +78,7 @@ __global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, i
       const int cnt = min(KS_IC, iend_all - i0);
       for (int ii = 0; ii < cnt; ++ii) {
         for (int l = 0; l < KL; ++l) {
-          const u64 kv = ksk[((size_t)(i0 + ii) * KL + l) * (n + 1) + col];
+          const u64 kv = ks_round(ksk[((size_t)(i0 + ii) * KL + l) * (n + 1) + col], R);
           const uint32_t kl = (uint32_t)kv, kh = (uint32_t)(kv >> 32);
           const uint32_t* d4 = (const uint32_t*)&dig[ii][l][0];
 #pragma unroll
@@ -103,12 +111,12 @@ __global__ void __launch_bounds__(256) k_keyswitch(const u64* __restrict__ in, i
   }
 }
 
-// colsum[t] = sum over all KSK rows of KSK[row][t] (mod 2^64)
-__global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, u64* __restrict__ colsum) {
+// colsum[t] = sum over all KSK rows of the rounded KSK[row][t] (mod 2^64)
+__global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, int R, u64* __restrict__ colsum) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t > n) return;
   u64 s = 0;
-  for (int r = 0; r < rows; ++r) s += ksk[(size_t)r * (n + 1) + t];
+  for (int r = 0; r < rows; ++r) s += ks_round(ksk[(size_t)r * (n + 1) + t], R);
   colsum[t] = s;
 }
 
@@ -119,33 +127,33 @@ __global__ void k_ksk_colsum(const u64* __restrict__ ksk, int rows, int n, u64* 
 // ---- key switch on the i8 matrix cores (v_mfma_i32_16x16x64_i8) ----------
 // out[c] = (0, .., 0, b'[c]) - sum_r D[c][r] * KSK[r], r = i * ks_level + l,
 // a GEMM [count x K] (digits in [-2^(b-1), 2^(b-1))) x [K x (n+1)] over
-// Z_2^64. The key is split into 8 balanced radix-256 byte planes,
-// KSK = sum_q s_q 2^(8q) with s_q in [-128, 127], each an i8 GEMM with i32
-// accumulation (|sum| <= K * 2^(b-1) * 128 < 2^31); the epilogue recombines
-// sum_q acc_q << 8q modulo 2^64 (exact: DESIGN.md §4.3).
+// Z_2^64. The rounded key (ks_round) is split into QP = 8 - R / 8 balanced
+// radix-256 byte planes, KSK = sum_q s_q 2^(R + 8q) with s_q in [-128, 127],
+// each an i8 GEMM with i32 accumulation (|sum| <= K * 2^(b-1) * 128 < 2^31);
+// the epilogue recombines sum_q acc_q << (R + 8q) modulo 2^64 (exact:
+// DESIGN.md §4.3).
 // Fragment layouts (checked by tools/mfma_i8_probe.hip): lane l holds
 // A[row l&15][k = 16 (l>>4) + j] and B[k = 16 (l>>4) + j][col l&15] in byte j;
 // C/D: row 4 (l>>4) + reg, col l&15.
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int KSM_NB_COLS = 16;  // columns per block
 
-// key planes: [kb][nb][q][lane][16 B]. The GEMM's K runs level-major,
+// key planes: [kb][nb][q][lane][16 B], q < QP. The GEMM's K runs level-major,
 // k = l * big + i (a k-block of 64 is 64 consecutive input coefficients of
 // one level, for any ks_level); the KSK itself is stored [i][l][n+1].
-__global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int big, int levels, int n1, int NB,
+__global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int big, int levels, int n1, int NB, int R, int QP,
                             int8_t* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)K * NB * 16) return;
   const int row = (int)(e / (NB * 16)), col = (int)(e % (NB * 16));
   const int l = row / big, i = row - l * big;
-  u64 x = col < n1 ? ksk[((size_t)i * levels + l) * n1 + col] : 0;
+  u64 x = col < n1 ? ks_round(ksk[((size_t)i * levels + l) * n1 + col], R) >> R : 0;
   const int kb = row >> 6, g = (row >> 4) & 3, j = row & 15;
   const int nb = col >> 4, lane = (col & 15) + 16 * g;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < QP; ++q) {
     const int8_t sq = (int8_t)(x & 0xff);
     x = (x - (u64)(int64_t)sq) >> 8;
-    out[((((size_t)kb * NB + nb) * 8 + q) * 64 + lane) * 16 + j] = sq;
+    out[((((size_t)kb * NB + nb) * QP + q) * 64 + lane) * 16 + j] = sq;
   }
 }
 
@@ -197,113 +205,135 @@ __global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, i
   }
 }
 
-// workgroup = 4 waves = 128 ciphertexts x 16 columns x 8 byte planes: each
-// wave two 16-ciphertext groups, so every key fragment read from LDS feeds two
-// MFMAs (one per group: with one, the four waves' fragment reads, 1 KB per
-// MFMA, saturate the LDS). The key tile of each k-block (8 KB) is shared
-// through LDS; the tiles and the digit fragments stream through a register
-// ring 4 k-blocks deep (the loads of k-block k + 4 are issued at k-block k;
-// the compiler counts their vmcnt), and the tiles pass through 3 LDS buffers
-// of two k-blocks each with one barrier per two k-blocks: the next step's
-// tiles are written while the slowest wave may still read the previous
-// step's (one barrier per k-block: 81.3 vs 76.2 us per 1024 ciphertexts at
-// (3,5)). KB % 4 == 0 for every supported parameter set (kN / 64 is a
-// multiple of 4).
+// workgroup = 4 waves = 128 ciphertexts x CB * 16 columns x QP byte planes x
+// one slice of K: each wave two 16-ciphertext groups, so every key fragment
+// read from LDS feeds two MFMAs (one per group: with one, the four waves'
+// fragment reads, 1 KB per MFMA, saturate the LDS). The key tile of each
+// k-block (CB * QP KB) is shared through LDS; the tiles and the digit
+// fragments stream through a register ring 4 k-blocks deep (the loads of
+// k-block k + 4 are issued at k-block k; the compiler counts their vmcnt),
+// and the tiles pass through 3 LDS buffers of two k-blocks each with one
+// barrier per two k-blocks: the next step's tiles are written while the
+// slowest wave may still read the previous step's (one barrier per k-block:
+// 81.3 vs 76.2 us per 1024 ciphertexts at (3,5), 8 planes). KB % 4 == 0 for
+// every supported parameter set (kN / 64 is a multiple of 4).
+// The digit fragments are the stream that bounds it: every column group
+// re-reads all of D, so a 16-column tile of 3 planes (the rounded key) ran no
+// faster than 8 planes (85 vs 80 us, docs/AB_LOG_r06.md); CB = 3 column
+// blocks per workgroup read D a third as often, and the K range split over
+// S workgroups (slice kslice k-blocks each, partial sums added with 64-bit
+// vector atomics into a zeroed output: exact and order-independent modulo
+// 2^64) keeps ~2 workgroups per CU at 1024 ciphertexts.
 constexpr int KSM_RING = 4, KSM_CTS = 128;  // ciphertexts per workgroup
-__global__ void __launch_bounds__(256) k_keyswitch_mfma(const v4i* __restrict__ D, const v4i* __restrict__ K8,
+template <int QP, int CB>
+__global__ void __launch_bounds__(256, 2) k_keyswitch_mfma(const v4i* __restrict__ D, const v4i* __restrict__ K8,
                                                         const u64* __restrict__ body, int64_t count, int n1, int NB,
-                                                        int KB, u64* __restrict__ out) {
+                                                        int KB, int R, int S, int kslice, u64* __restrict__ out) {
 #ifndef FHEICP_KS_KP
 #define FHEICP_KS_KP 2  // k-blocks per barrier (1: one barrier per k-block, A/B builds)
 #endif
   constexpr int KP = FHEICP_KS_KP;
-  __shared__ v4i bt[3][KP][8 * 64];
+  constexpr int TV = CB * QP * 64;          // v4i per key tile (one k-block, CB column blocks)
+  constexpr int TL = (TV + 255) / 256;      // tile words per thread
+  __shared__ v4i bt[3][KP][TV];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // XCD-aware order over the (ciphertext block, column block) grid: block b
-  // runs on XCD b % 8, and each XCD takes a contiguous run of column blocks
-  // with all their ciphertext blocks, so a column block's key tiles come
-  // into one XCD's L2 once for every block (the blocks of one column block
-  // dispatched round-robin over the XCDs made each XCD stream the whole key)
+  // XCD-aware order over the (column group, ciphertext block, K slice) grid:
+  // block b runs on XCD b % 8, and each XCD takes a contiguous run of column
+  // groups with all their ciphertext blocks and slices, so a column group's
+  // key tiles come into one XCD's L2 once for every block (the blocks of one
+  // column block dispatched round-robin over the XCDs made each XCD stream
+  // the whole key)
   const int nblk = (int)gridDim.x, bid = (int)blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int ngrp = nblk / NB;
-  const int nb = t / ngrp;
-  const int64_t ncb = (count + 15) / 16;                         // 16-ciphertext groups (digit rows)
-  const int64_t cb0 = (int64_t)(t - nb * ngrp) * (KSM_CTS / 16) + 2 * w;
+  const int NG = NB / CB;                   // column groups (NB padded to a multiple of CB)
+  const int per = nblk / NG;                // ciphertext blocks x slices per column group
+  const int ng = t / per, rest = t - ng * per, ctb = rest / S, sl = rest - ctb * S;
+  const int kb_lo = sl * kslice, kb_hi = min(KB, kb_lo + kslice);
+  const int64_t ncb = (count + 15) / 16;   // 16-ciphertext groups (digit rows)
+  const int64_t cb0 = (int64_t)ctb * (KSM_CTS / 16) + 2 * w;
   // a group past the batch streams group 0's digits and stores nothing
   const v4i* Dv0 = D + (size_t)(cb0 < ncb ? cb0 : 0) * KB * 64 + lane;
   const v4i* Dv1 = D + (size_t)(cb0 + 1 < ncb ? cb0 + 1 : 0) * KB * 64 + lane;
-  const v4i* Kv = K8 + (size_t)nb * 8 * 64;
-  const size_t kstride = (size_t)NB * 8 * 64;  // v4i per k-block of the key
-  v4i acc[2][8];
+  const v4i* Kv = K8 + (size_t)ng * TV;
+  const size_t kstride = (size_t)NB * QP * 64;  // v4i per k-block of the key
+  v4i acc[2][CB][QP];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[h][q] = (v4i){0, 0, 0, 0};
-  v4i rk[KSM_RING][2], rd[KSM_RING][2];
-  // prologue: k-blocks 0..3 in flight, the first step's tiles into LDS
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int q = 0; q < QP; ++q) acc[h][c][q] = (v4i){0, 0, 0, 0};
+  v4i rk[KSM_RING][TL], rd[KSM_RING][2];
+  auto tile_load = [&](v4i(&r)[TL], int kb) {
+#pragma unroll
+    for (int e = 0; e < TL; ++e)
+      if (e * 256 + tid < TV) r[e] = Kv[kb * kstride + e * 256 + tid];
+  };
+  auto tile_store = [&](v4i* dst, const v4i(&r)[TL]) {
+#pragma unroll
+    for (int e = 0; e < TL; ++e)
+      if (e * 256 + tid < TV) dst[e * 256 + tid] = r[e];
+  };
+  // prologue: k-blocks lo..lo+3 in flight, the first step's tiles into LDS
 #pragma unroll
   for (int j = 0; j < KSM_RING; ++j) {
-    rk[j][0] = Kv[j * kstride + tid];
-    rk[j][1] = Kv[j * kstride + tid + 256];
-    rd[j][0] = Dv0[(size_t)j * 64];
-    rd[j][1] = Dv1[(size_t)j * 64];
+    tile_load(rk[j], kb_lo + j);
+    rd[j][0] = Dv0[(size_t)(kb_lo + j) * 64];
+    rd[j][1] = Dv1[(size_t)(kb_lo + j) * 64];
   }
 #pragma unroll
-  for (int h = 0; h < KP; ++h) {
-    bt[0][h][tid] = rk[h][0];
-    bt[0][h][tid + 256] = rk[h][1];
-  }
+  for (int h = 0; h < KP; ++h) tile_store(bt[0][h], rk[h]);
   // steps of KP k-blocks, one barrier each; the ring slots of a step's
   // k-blocks (in LDS since the previous step) reload k-block k + 4, and the
   // next step's tiles (loaded one or two steps ago) go into its LDS buffer
-  for (int kb = 0; kb < KB; kb += KSM_RING) {
+  for (int kb = kb_lo; kb < kb_hi; kb += KSM_RING) {
 #pragma unroll
     for (int j0 = 0; j0 < KSM_RING; j0 += KP) {
-      const int k0 = kb + j0, step = k0 / KP;
+      const int k0 = kb + j0, step = (k0 - kb_lo) / KP;
 #pragma unroll
-      for (int h = 0; h < KP; ++h) {
-        const int kn = min(k0 + h + KSM_RING, KB - 1);  // clamped at the end: reloads, no branch
-        rk[j0 + h][0] = Kv[kn * kstride + tid];
-        rk[j0 + h][1] = Kv[kn * kstride + tid + 256];
-      }
-      if (k0 + KP < KB) {
+      for (int h = 0; h < KP; ++h) tile_load(rk[j0 + h], min(k0 + h + KSM_RING, kb_hi - 1));  // clamped: reloads
+      if (k0 + KP < kb_hi) {
 #pragma unroll
-        for (int h = 0; h < KP; ++h) {
-          const int j1 = (j0 + KP + h) % KSM_RING;
-          bt[(step + 1) % 3][h][tid] = rk[j1][0];
-          bt[(step + 1) % 3][h][tid + 256] = rk[j1][1];
-        }
+        for (int h = 0; h < KP; ++h) tile_store(bt[(step + 1) % 3][h], rk[(j0 + KP + h) % KSM_RING]);
       }
       __syncthreads();
 #pragma unroll
       for (int h = 0; h < KP; ++h) {
         const v4i a0 = rd[j0 + h][0], a1 = rd[j0 + h][1];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const v4i bq = bt[step % 3][h][q * 64 + lane];
-          acc[0][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq, acc[0][q], 0, 0, 0);
-          acc[1][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq, acc[1][q], 0, 0, 0);
-        }
-        const int kn = min(k0 + h + KSM_RING, KB - 1);
+        for (int c = 0; c < CB; ++c)
+#pragma unroll
+          for (int q = 0; q < QP; ++q) {
+            const v4i bq = bt[step % 3][h][(c * QP + q) * 64 + lane];
+            acc[0][c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bq, acc[0][c][q], 0, 0, 0);
+            acc[1][c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bq, acc[1][c][q], 0, 0, 0);
+          }
+        const int kn = min(k0 + h + KSM_RING, kb_hi - 1);
         rd[j0 + h][0] = Dv0[(size_t)kn * 64];
         rd[j0 + h][1] = Dv1[(size_t)kn * 64];
       }
     }
   }
-  const int col = nb * KSM_NB_COLS + (lane & 15);
-  if (col >= n1) return;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (cb0 + h >= ncb) continue;
+  for (int c = 0; c < CB; ++c) {
+    const int col = (ng * CB + c) * KSM_NB_COLS + (lane & 15);
+    if (col >= n1) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t c = (cb0 + h) * 16 + 4 * (lane >> 4) + r;
-      if (c >= count) continue;
-      u64 v = 0;
+    for (int h = 0; h < 2; ++h) {
+      if (cb0 + h >= ncb) continue;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v += (u64)(int64_t)acc[h][q][r] << (8 * q);
-      out[(size_t)c * n1 + col] = (col == n1 - 1 ? body[c] : (u64)0) - v;
+      for (int r = 0; r < 4; ++r) {
+        const int64_t ci = (cb0 + h) * 16 + 4 * (lane >> 4) + r;
+        if (ci >= count) continue;
+        u64 v = 0;
+#pragma unroll
+        for (int q = 0; q < QP; ++q) v += (u64)(int64_t)acc[h][c][q][r] << (R + 8 * q);
+        const u64 o = (col == n1 - 1 && sl == 0 ? body[ci] : (u64)0) - v;
+        if (S == 1)
+          out[(size_t)ci * n1 + col] = o;
+        else
+          atomicAdd((unsigned long long*)&out[(size_t)ci * n1 + col], (unsigned long long)o);
+      }
     }
   }
 }

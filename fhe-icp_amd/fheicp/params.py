@@ -439,6 +439,14 @@ def _tuniform_var(b: int) -> float:
     return (2.0 ** (2 * b + 1) + 1.0) / 6.0
 
 
+def ks_round_bits(p: SchemeParams) -> int:
+    """The key switch rounds every KSK word to a multiple of 2^R (fheicp.hip
+    ks_round_bits, oracle/tfhe_ref.c): R = 8 floor((lwe_noise_bits - 6) / 8),
+    at most 40, so the rounding stays below 2^-7 of the KSK noise and the i8
+    matrix-core key switch needs 8 - R / 8 byte planes."""
+    return 0 if p.lwe_noise_bits < 14 else 8 * min((p.lwe_noise_bits - 6) // 8, 5)
+
+
 def _variances(p: SchemeParams, group: int = 1):
     """(bootstrap, key switch, modulus switch) output variances, relative to
     the 2^64 torus, for the main gadget of p on the classic
@@ -449,7 +457,8 @@ def _variances(p: SchemeParams, group: int = 1):
     output roundings."""
     q2 = 2.0 ** 128
     s2_bsk = _tuniform_var(p.glwe_noise_bits) / q2
-    s2_ksk = _tuniform_var(p.lwe_noise_bits) / q2
+    R = ks_round_bits(p)
+    s2_ksk = (_tuniform_var(p.lwe_noise_bits) + (2.0 ** (2 * R) / 12.0 if R else 0.0)) / q2
     B = 2.0 ** p.pbs_base_log
     rows = p.pbs_level * (p.k + 1) * p.N
     steps = p.n * (1 + p.k * p.N / 2)

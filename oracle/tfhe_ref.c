@@ -574,8 +574,20 @@ static void decompose_ks(uint64_t x, int bl, int L, int64_t* d) {
 }
 void ref_decompose_ks(uint64_t x, int bl, int L, int64_t* d) { decompose_ks(x, bl, L, d); }
 
+/* The key switch uses each KSK word rounded to the nearest multiple of 2^R,
+ * R = 8 floor((lwe_noise_bits - 6) / 8) (at most 40, 0 below 14 bits): the
+ * rounding error is below 2^-7 of the KSK's TUniform noise, and the GPU's i8
+ * matrix-core key switch needs 8 - R / 8 byte planes of it (libfheicp
+ * ks_round_bits / k_server.h ks_round). */
+static int ks_round_bits(const ref_params* P) {
+  if (P->lwe_noise_bits < 14) return 0;
+  const int r = (P->lwe_noise_bits - 6) / 8;
+  return 8 * (r < 5 ? r : 5);
+}
+static uint64_t ks_round(uint64_t x, int R) { return R ? (x + (1ull << (R - 1))) & ~((1ull << R) - 1) : x; }
+
 static void keyswitch1(const ref_params* P, const uint64_t* ksk, const uint64_t* in, uint64_t* out) {
-  const int n = P->n, dimb = P->k * P->N, KL = P->ks_level;
+  const int n = P->n, dimb = P->k * P->N, KL = P->ks_level, R = ks_round_bits(P);
   int64_t d[64];
   for (int t = 0; t < n; ++t) out[t] = 0;
   out[n] = in[dimb];
@@ -585,7 +597,7 @@ static void keyswitch1(const ref_params* P, const uint64_t* ksk, const uint64_t*
       if (!d[l]) continue;
       const uint64_t* row = ksk + ((size_t)i * KL + l) * (n + 1);
       const uint64_t dd = (uint64_t)d[l];
-      for (int t = 0; t <= n; ++t) out[t] -= dd * row[t];
+      for (int t = 0; t <= n; ++t) out[t] -= dd * ks_round(row[t], R);
     }
   }
 }

@@ -401,6 +401,41 @@ def test_keyswitch_digits_zero_mean(oracle_lib, beta, lvl):
     assert abs((ds.astype(float) ** 2).mean() / ((B * B + 2) / 12) - 1) < 0.02
 
 
+def test_keyswitch_uses_the_rounded_key(toy_ref):
+    """The key switch's definition (tfhe_ref.c keyswitch1, k_server.h
+    ks_round): every KSK word rounded to the nearest multiple
+    of 2^R, R = params.ks_round_bits (40 at lwe_noise_bits = 46: 3 byte planes
+    on the matrix cores). Restated here in Python integers on 3 TOY
+    ciphertexts, bit-exact; the exact key gives a different result that
+    differs only far below the key-switch noise."""
+    from fheicp.params import ks_round_bits
+    from oracle.tfhe_ref import decompose_ks
+    p = TOY
+    R = ks_round_bits(p)
+    assert R == 40 and ks_round_bits(params_for_bits(16)) == 40
+    M = 2 ** 64
+    rnd = lambda x: ((x + (1 << (R - 1))) >> R << R) % M
+    big, n, KL = p.k * p.N, p.n, p.ks_level
+    ksk = toy_ref.ksk.reshape(big, KL, n + 1)
+    ct = toy_ref.encrypt_ints(np.array([-77, 0, 91], np.int64), seed=12)
+    got = toy_ref.keyswitch(ct)
+    for c in range(ct.shape[0]):
+        out = [0] * n + [int(ct[c, big])]
+        exact = list(out)
+        for i in range(big):
+            d = decompose_ks(int(ct[c, i]), p.ks_base_log, KL)
+            for l in range(KL):
+                if d[l]:
+                    row = ksk[i, l]
+                    for t in range(n + 1):
+                        out[t] = (out[t] - int(d[l]) * rnd(int(row[t]))) % M
+                        exact[t] = (exact[t] - int(d[l]) * int(row[t])) % M
+        assert [int(x) for x in got[c]] == out
+        assert exact != out
+        diff = [((a - b + M // 2) % M) - M // 2 for a, b in zip(out, exact)]
+        assert max(abs(x) for x in diff) < 2 ** (R + 10)
+
+
 def test_oracle_sign_entry_points_under_sanitizers(tmp_path):
     """ref_sign_extract / ref_sign_extract3 pass short key arrays
     to ref_sign_extract_keys, which reads one slot per gadget (NGAD - 1). The

@@ -15,7 +15,7 @@ import json; d=json.loads(open('$o').read().strip().splitlines()[-1])
 p=d.get('parity',{})
 print('${TAG:-c2} $t rep$rep', d['value'], d['ms_per_step'], 'parity', all(v for k,v in p.items() if isinstance(v,bool)),
       ' '.join(f\"{k}:{v.get('kernel')}={v.get('avg_launch_ms')}\" for k,v in d['roofline'].get('kernels',{}).items()),
-      'leveled', d['leveled_score']['roofline']['avg_launch_ms'])
+      'leveled', d['leveled_score']['roofline']['avg_launch_ms'], 'ks_ms_total', d.get('keyswitch_ms_total'))
 "
   done
 done
