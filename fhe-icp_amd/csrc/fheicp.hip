@@ -1033,7 +1033,6 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
     u64* body = (u64*)((char*)ws + dbytes);
     hipEvent_t e1;
     prof_begin(ctx, ctx->prof_ks, st, &e1);
-    ctx->prof_ks.kernel = "k_keyswitch_mfma";
     hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)(p.k * p.N / 64), (unsigned)ncb), dim3(256), 0, st, d_big, count,
                        p.k * p.N, p.ks_base_log, p.ks_level, shift, add_body, KB, D, body);
     const int R = ks_round_bits(p);
@@ -1046,6 +1045,7 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
     if (S > 1) HIPCHK(ctx, hipMemsetAsync(d_small, 0, 8 * (size_t)count * n1, st));
     const dim3 gks((unsigned)(tiles * S));
 #define KSM(Q, C)                                                                                                    \
+  ctx->prof_ks.kernel = "k_keyswitch_mfma<" #Q ", " #C ">";                                                         \
   hipLaunchKernelGGL((k_keyswitch_mfma<Q, C>), gks, dim3(256), 0, st, (const v4i*)D, (const v4i*)ctx->ksk8, body,    \
                      count, n1, NB, KB, R, S, kslice, d_small)
     switch ((8 - R / 8) * 4 + CB) {

@@ -100,21 +100,47 @@ def test_linear_and_keyswitch_bit_exact(which, request):
         assert np.array_equal(u64(ks), ks_ref), f"keyswitch shift={shift}"
 
 
-@pytest.mark.parametrize("B", [1, 17, 300])
+@pytest.mark.parametrize("B", [1, 17, 300, 1024, 2000])
 def test_keyswitch_ragged_batches_bit_exact(real, B):
-    """The MFMA key switch (k_keyswitch_mfma: 128 ciphertexts per workgroup,
-    two 16-ciphertext groups per wave, a 4-deep load ring) on batches that
-    leave idle waves and half-empty groups: bit-exact against the oracle."""
+    """The MFMA key switch (k_keyswitch_mfma: 128 ciphertexts x 48 columns per
+    workgroup, two 16-ciphertext groups per wave, a 4-deep load ring, K split
+    over S workgroups: S = 20, 20, 8, 3 and 1 for these batches) on batches
+    that leave idle waves and half-empty groups: bit-exact against the
+    oracle's key switch on the rounded KSK."""
     eng, ref = real
     P = eng.msg_bits
     rng = np.random.default_rng(60 + B)
     v = rng.integers(-(2 ** (P - 1)), 2 ** (P - 1), B)
     ct = eng.encrypt(v, seed=61, id0=7 * B)
     ct_ref = ref.encrypt_ints(v, seed=61, id0=7 * B)
+    eng.profile(True)
     ks = eng.keyswitch(ct, 2, 1 << 61)
+    eng.profile(False)
     sh = ct_ref << np.uint64(2)
     sh[:, -1] += np.uint64(1 << 61)
     assert np.array_equal(u64(ks), ref.keyswitch(sh))
+    # three byte planes of the rounded KSK, three column blocks per workgroup
+    assert eng.kernel_name("keyswitch") == "k_keyswitch_mfma<3, 3>"
+
+
+def test_keyswitch_valu_variant_bit_exact(need_gpu, oracle_lib, monkeypatch):
+    """The VALU split-K key switch (k_keyswitch, the path for parameter sets
+    the i8 matrix cores cannot take; FHEICP_KS_VARIANT=1 forces it) reads the
+    same rounded KSK words (ks_round) and its colsum: bit-exact against the
+    oracle, like the MFMA form."""
+    monkeypatch.setenv("FHEICP_KS_VARIANT", "1")
+    eng = Engine(TOY, 0)
+    eng.keygen(4242)
+    ref = oracle_lib.RefTFHE(TOY.as_dict(), 4242)
+    v = np.random.default_rng(62).integers(-128, 128, 70)
+    ct = eng.encrypt(v, seed=63)
+    sh = ref.encrypt_ints(v, seed=63) << np.uint64(3)
+    sh[:, -1] += np.uint64(1 << 60)
+    assert np.array_equal(u64(eng.keyswitch(ct, 3, 1 << 60)), ref.keyswitch(sh))
+    eng.profile(True)
+    eng.keyswitch(ct, 0, 0)
+    eng.profile(False)
+    assert eng.kernel_name("keyswitch") == "k_keyswitch"
 
 
 def test_pbs_matches_oracle_toy(toy):
