@@ -1031,19 +1031,23 @@ static int keyswitch_lane(fhe_ctx* ctx, const uint64_t* d_big, int64_t count, in
     void* ws = lane ? ctx->ks_ws1 : ctx->ks_ws;
     uint32_t* D = (uint32_t*)ws;
     u64* body = (u64*)((char*)ws + dbytes);
-    hipEvent_t e1;
-    prof_begin(ctx, ctx->prof_ks, st, &e1);
-    hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)(p.k * p.N / 64), (unsigned)ncb), dim3(256), 0, st, d_big, count,
-                       p.k * p.N, p.ks_base_log, p.ks_level, shift, add_body, KB, D, body);
     const int R = ks_round_bits(p);
     // K split over S workgroups when the (ciphertext block, column group)
-    // grid alone would leave CUs idle: ~2 workgroups per CU
-    const int64_t ctb = (count + KSM_CTS - 1) / KSM_CTS, tiles = ctb * (NB / CB);
-    int S = (int)std::max<int64_t>(1, std::min<int64_t>(KB / KSM_RING, 512 / tiles));
+    // grid alone would leave CUs idle: ~2 workgroups per CU (S = 3 at 1024
+    // ciphertexts; 1, 2, 4-12 measured slower there, tools/ks_sweep.py)
+    const int64_t ctb = (count + KSM_CTS - 1) / KSM_CTS, ktiles = ctb * (NB / CB);
+    int S = (int)std::max<int64_t>(1, std::min<int64_t>(KB / KSM_RING, 512 / ktiles));
+#ifdef FHEICP_KS_AB  // A/B builds only: the split forced (tools/build_variant.sh)
+    if (const char* e = getenv("FHEICP_KS_S")) S = std::max(1, std::min(KB / KSM_RING, atoi(e)));
+#endif
     const int kslice = (KB / KSM_RING + S - 1) / S * KSM_RING;
     S = (KB + kslice - 1) / kslice;
-    if (S > 1) HIPCHK(ctx, hipMemsetAsync(d_small, 0, 8 * (size_t)count * n1, st));
-    const dim3 gks((unsigned)(tiles * S));
+    hipEvent_t e1;
+    prof_begin(ctx, ctx->prof_ks, st, &e1);
+    // the digits kernel also zeroes the output the split's atomics add into
+    hipLaunchKernelGGL(k_ks_digits, dim3((unsigned)(p.k * p.N / 64), (unsigned)ncb), dim3(256), 0, st, d_big, count,
+                       p.k * p.N, p.ks_base_log, p.ks_level, shift, add_body, KB, D, body, S > 1 ? n1 : 0, d_small);
+    const dim3 gks((unsigned)(ktiles * S));
 #define KSM(Q, C)                                                                                                    \
   ctx->prof_ks.kernel = "k_keyswitch_mfma<" #Q ", " #C ">";                                                         \
   hipLaunchKernelGGL((k_keyswitch_mfma<Q, C>), gks, dim3(256), 0, st, (const v4i*)D, (const v4i*)ctx->ksk8, body,    \

@@ -162,13 +162,25 @@ __global__ void k_ksk_to_i8(const u64* __restrict__ ksk, int K, int big, int lev
 // consecutive coefficients of one ciphertext and writes one packed word (4
 // digits, one byte each) per level; grid (big / 64, ceil(count / 16)), 256
 // threads: 16 ciphertexts x 64 coefficients. Needs big % 64 == 0,
-// levels <= 8 and levels * beta <= 32 (fhe_ctx_create).
+// levels <= 8 and levels * beta <= 32 (fhe_ctx_create). With zero_n1 > 0 it
+// also zeroes the key switch's output rows of its 16 ciphertexts (zero_n1
+// words each, a slice of columns per block), for the split-K atomics of
+// k_keyswitch_mfma (one launch fewer than a memset).
 __global__ void __launch_bounds__(256) k_ks_digits(const u64* __restrict__ in, int64_t count, int big, int beta,
                                                    int levels, int shift, u64 add_body, int KB,
-                                                   uint32_t* __restrict__ D, u64* __restrict__ body) {
+                                                   uint32_t* __restrict__ D, u64* __restrict__ body, int zero_n1,
+                                                   u64* __restrict__ zero_out) {
   const int t = threadIdx.x, cl = t >> 4, iq = t & 15;
   const int64_t cb = blockIdx.y, c = cb * 16 + cl;
   const int i0 = blockIdx.x * 64 + iq * 4;
+  if (zero_n1 > 0) {
+    const int per = (zero_n1 + (int)gridDim.x - 1) / (int)gridDim.x;
+    for (int e = t; e < 16 * per; e += 256) {
+      const int q = e / per, col = (int)blockIdx.x * per + (e - q * per);
+      const int64_t cz = cb * 16 + q;
+      if (cz < count && col < zero_n1) zero_out[(size_t)cz * zero_n1 + col] = 0;
+    }
+  }
   if (c >= count) return;
   const u64* src = in + (size_t)c * (big + 1);
   if (blockIdx.x == 0 && iq == 0) body[c] = (src[big] << shift) + add_body;
