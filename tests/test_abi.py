@@ -332,3 +332,11 @@ def test_table_gadget_matches_params():
     assert L.fhe_pbs_table_gadget(C.byref(_lib.params_struct(TOY.as_dict()))) == table_gadget(TOY) == 0
     bad = _lib.params_struct(dict(TOY.as_dict(), N=1000))
     assert L.fhe_pbs_table_gadget(C.byref(bad)) == -1
+
+
+def test_integration_guide_names_every_entry_point():
+    """INTEGRATION.md's ABI table covers every function the headers declare
+    (the guide a maintainer binds from stays in step with the library)."""
+    text = (Path(__file__).resolve().parents[1] / "INTEGRATION.md").read_text()
+    missing = [n for n in declared_functions() if n not in text]
+    assert not missing, missing
